@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""bench.py — Mrays/s (primary + bounces) of the gfx950 render path.
+
+Default workload (BASELINE.json configs[1], C2): big_scene1 (the reference's random-spheres
+scene, scenes.h:140-222), 1200x800, 100 rays per pixel split like the reference's main.cu as
+no_fb = 10 frame buffers x 10 samples_per_pixel_per_fb (render.h:36-38), depth 50, seed 1984,
+reference camera-RNG mode.  One step = one draw(): render_init + all 10 fb renders + per-fb
+quantise/average (resolve) [+ the RCCL gather of the 8-bit rows to rank 0 when N > 1].
+A ray segment = one top-level world query (render.h:63), counted on the device.
+
+N > 1 (one process per GPU, torch.distributed over RCCL): rows are dealt in 8-row bands
+round-robin over ranks; each rank renders and resolves its rows for every fb; one all-gather of
+the 8-bit rows assembles the image.  Strong scaling (the image is fixed).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
+NODE_BYTES = 32         # rt_bvh_node
+PRIM_BYTES = 48         # rt_prim
+ITEM_BYTES = 32 + 12    # per (fb, pixel): RNG state read + fb write
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="big1")
+    ap.add_argument("--width", type=int, default=1200)
+    ap.add_argument("--height", type=int, default=800)
+    ap.add_argument("--spp", type=int, default=10, help="samples_per_pixel_per_fb")
+    ap.add_argument("--nfb", type=int, default=10, help="no_fb")
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--cam", choices=["ref", "per_pixel"], default="ref")
+    ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stats", action="store_true", help="skip the untimed node/prim counting pass")
+    ap.add_argument("--png", default="", help="write the assembled image (rank 0)")
+    return ap.parse_args()
+
+
+def cpu_baseline(a, budget_s: float) -> dict:
+    """The CPU oracle (C++ restatement of the reference render path) on the host's cores, over a
+    bounded sample of the same workload: every k-th row, all fbs."""
+    from oracle import ref_cpu
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    sc = ref_cpu.RefScene(a.scene)
+    cam = 0 if a.cam == "ref" else 1
+    # calibrate on one row of fb 0
+    t0 = time.perf_counter()
+    _, c, _ = sc.render(a.width, a.height, a.spp, 0, a.depth, cam, rows=(a.height // 2, a.height), threads=threads)
+    t1 = time.perf_counter() - t0
+    per_row_fb = max(t1, 1e-4)
+    nrows = max(1, min(a.height, int(budget_s / (per_row_fb * a.nfb))))
+    stride = max(1, a.height // nrows)
+    segs = 0
+    t0 = time.perf_counter()
+    for f in range(a.nfb):
+        _, c, _ = sc.render(a.width, a.height, a.spp, f, a.depth, cam, rows=(0, stride), threads=threads)
+        segs += c["segments"]
+    dt = time.perf_counter() - t0
+    rows = len(range(0, a.height, stride))
+    return {"value": segs / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{a.scene} {a.width}x{a.height}, rows 0::{stride} ({rows} rows) x {a.nfb} fb x {a.spp} spp, "
+                      f"{segs} segments in {dt:.1f} s, {threads} threads (oracle/ref_cpu.cpp, g++ -O2)"}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    import raytracing_gpu_amd as rt
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+
+    ctx = rt.Context(local)
+    sc = rt.Scene.builtin(a.scene)
+    ctx.upload(sc)
+    cam = rt.RT_CAM_REF_SLOT0 if a.cam == "ref" else rt.RT_CAM_PER_PIXEL
+    args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, band_rows=a.band_rows,
+                        band_first=rank, band_stride=world)
+    rows = rt.owned_rows(args)
+    all_rows = []
+    for r in range(world):
+        ar = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, band_rows=a.band_rows,
+                          band_first=r, band_stride=world)
+        all_rows.append(rt.owned_rows(ar))
+    max_rows = max(len(x) for x in all_rows)
+    fb = torch.empty(a.nfb * len(rows) * a.width * 3, dtype=torch.float32, device=dev)
+    img = torch.zeros(max_rows * a.width * 3, dtype=torch.uint8, device=dev)
+    gathered = torch.empty(world * img.numel(), dtype=torch.uint8, device=dev) if world > 1 else None
+
+    stats = None
+    if not a.no_stats:  # untimed pass of the counting variant: node / prim tests for B_seg
+        ctx.render_init(a.width, a.height, 1984)
+        sargs = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, band_rows=a.band_rows,
+                             band_first=rank, band_stride=world, stats=True)
+        stats = ctx.render(sargs, fb.data_ptr())
+
+    seg_step = [0]
+    kms = []
+
+    def step():
+        ctx.render_init(a.width, a.height, 1984)
+        cnt = ctx.render(args, fb.data_ptr())
+        kms.append(ctx.last_render_ms())
+        ctx.resolve(args, fb.data_ptr(), img.data_ptr())
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, img)
+        seg_step[0] = cnt["segments"]
+        return cnt
+
+    for _ in range(a.warmup):
+        step()
+    kms.clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+
+    tot = torch.tensor([float(seg_step[0])], dtype=torch.float64, device=dev)
+    tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    segs = float(tot.item())
+    dt = float(tmax.item())
+    value = segs * a.steps / dt / 1e6
+
+    if rank == 0:
+        avg_ms = sum(kms) / len(kms)
+        roof = None
+        if stats is not None:
+            items = a.nfb * len(rows) * a.width
+            bytes_launch = NODE_BYTES * stats["node_tests"] + PRIM_BYTES * stats["prim_tests"] + ITEM_BYTES * items
+            achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                    "kernel": "render_kernel", "kernel_avg_ms": round(avg_ms, 3),
+                    "bytes_per_launch": int(bytes_launch),
+                    "bytes_per_segment": round(bytes_launch / max(stats["segments"], 1), 2),
+                    "node_tests_per_segment": round(stats["node_tests"] / max(stats["segments"], 1), 3),
+                    "prim_tests_per_segment": round(stats["prim_tests"] / max(stats["segments"], 1), 3)}
+        out = {
+            "metric": "Mrays/sec (primary+bounces) on RTIOW random-spheres 1200x800x100spp",
+            "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (reference scene generator, seed 1984)",
+            "config": {"workload": f"C2 {a.scene} {a.width}x{a.height}, {a.nfb} fb x {a.spp} spp = "
+                                   f"{a.nfb * a.spp} rays/pixel, depth {a.depth}, cam {a.cam}",
+                       "scene": a.scene, "width": a.width, "height": a.height, "rays_per_pixel": a.nfb * a.spp,
+                       "no_fb": a.nfb, "spp_per_fb": a.spp, "max_depth": a.depth,
+                       "segments_per_step": int(segs), "parallelism": f"rows{world}"},
+            "roofline": roof,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(a, a.cpu_seconds)
+        print(json.dumps(out), flush=True)
+        if a.png:
+            import numpy as np
+
+            g = (gathered if world > 1 else img).cpu().numpy().reshape(world, max_rows, a.width, 3)
+            pic = np.zeros((a.height, a.width, 3), np.uint8)
+            for r in range(world):
+                for k, j in enumerate(all_rows[r]):
+                    pic[a.height - 1 - j] = g[r, k]
+            rt.write_png(a.png, pic)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

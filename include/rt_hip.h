@@ -1,0 +1,226 @@
+/* rt_hip.h — C ABI of the MI355X (gfx950) path-tracing hot path.
+ *
+ * Drop-in replacement for the per-pixel render path of daRoyalCacti/Raytracing_GPU:
+ *
+ *   rt_render_init   replaces  __global__ render_init(W, H, curandState*)        render.h:84-92
+ *   rt_render        replaces  __global__ render(fb, W, H, ns, cam, states, world,
+ *                                                max_depth, id, background)     render.h:94-113
+ *                              (and color_f, render.h:55-81, plus everything it calls:
+ *                               bvh.h:348-436, aabb.h:19-104, hittable_list.h:23-39,
+ *                               sphere.h, moving_sphere.h, aarect.h, box.h, hittable.h:31-143,
+ *                               constant_medium.h, material.h, texture.h, perlin.h)
+ *   rt_resolve       replaces  write_frame_buffer + average_images (the per-fb 8-bit quantise
+ *                              and square-average of draw())            color.h:19-170
+ *   rt_scene_upload  replaces  the device-side object graph that struct scene's constructor
+ *                              builds with <<<1,1>>> kernels            scenes.h:36-79
+ *   rt_draw          replaces  void draw(scene&, render_settings)       render.h:118-174
+ *
+ * Conventions (render.h:99): a frame buffer is row-major, p = j*W + i, j = 0 the BOTTOM row,
+ * 3 floats per pixel.  Every call returns 0 on success or a nonzero rt_status; rt_last_error()
+ * gives the message.  Nothing exits or throws across the boundary (the reference's
+ * checkCudaErrors -> exit(99), common.h:30-38, becomes a status code).  A context belongs to one
+ * device and one host thread at a time.  Calls are synchronous unless named _async.
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum rt_status {
+  RT_OK = 0,
+  RT_ERR_ARG = 1,     /* invalid argument / shape */
+  RT_ERR_HIP = 2,     /* HIP runtime error */
+  RT_ERR_STATE = 3,   /* call order (e.g. render before upload) */
+  RT_ERR_SCENE = 4,   /* malformed scene arrays */
+  RT_ERR_NOMEM = 5
+};
+
+/* ------------------------------------------------------------------ flattened scene (host) */
+/* Camera as built by camera::camera(), camera.h:18-47. */
+typedef struct rt_camera {
+  float origin[3], lower_left[3], horizontal[3], vertical[3];
+  float u[3], v[3], w[3];
+  float lens_radius, time0, time1;
+} rt_camera;
+
+enum rt_prim_type {
+  RT_PRIM_SPHERE = 0,        /* sphere.h          p = cx cy cz r                           */
+  RT_PRIM_MOVING_SPHERE = 1, /* moving_sphere.h   p = c0x c0y c0z r  dx dy dz t0  dt
+                                                  (d = center1-center0, dt = time1-time0)   */
+  RT_PRIM_RECT_XY = 2,       /* aarect.h xy_rect  p = x0 x1 y0 y1 k  (x1-x0) (y1-y0)        */
+  RT_PRIM_RECT_XZ = 3,       /* aarect.h xz_rect  p = x0 x1 z0 z1 k  (x1-x0) (z1-z0)        */
+  RT_PRIM_RECT_YZ = 4,       /* aarect.h yz_rect  p = y0 y1 z0 z1 k  (y1-y0) (z1-z0)        */
+  RT_PRIM_TRIANGLE = 5       /* triangle.h        p[0] = index into rt_scene_soa.triangles  */
+};
+/* 48-byte primitive record; three 16-byte loads on the device. */
+typedef struct rt_prim {
+  float p[10];
+  int32_t type;
+  int32_t material;
+} rt_prim;
+
+/* Triangle (triangle.h:19-41 constructor output), 128 bytes. */
+typedef struct rt_triangle {
+  float v0[3], e0[3], e1[3]; /* vertex0, vertex1-vertex0, vertex2-vertex0 */
+  float d00, d01, d11, inv_denom;
+  float uv[6];               /* u0 v0 u1 v1 u2 v2 */
+  float n0[3], n1[3], n2[3];
+  int32_t vertex_normals;
+  int32_t pad[2];
+} rt_triangle;
+
+/* Inner node of a reference-layout BVH (bvh.h:133-346): a perfect binary tree of `rows` inner
+ * levels stored in heap order (children of k are 2k+1, 2k+2).  Nodes of the last inner level
+ * carry the one or two primitives of their leaves in leaf_a / leaf_b (-1 = none). */
+typedef struct rt_bvh_node {
+  float lo[3];
+  int32_t leaf_a;
+  float hi[3];
+  int32_t leaf_b;
+} rt_bvh_node;
+
+enum rt_object_kind {
+  RT_OBJ_PRIM = 0,   /* a = prim index                                                         */
+  RT_OBJ_LIST = 1,   /* a = first prim, b = count; hittable_list semantics (box.h)             */
+  RT_OBJ_BVH = 2,    /* a = first node, b = rows (inner levels)                                */
+  RT_OBJ_XFORM = 3,  /* translate(rotate_y(child)), hittable.h:31-143; a = child object
+                        (PRIM/LIST/BVH), b = flags (1 translate, 2 rotate_y);
+                        f[0..2] = offset, f[3] = sin, f[4] = cos                               */
+  RT_OBJ_MEDIUM = 4  /* constant_medium.h; a = boundary object (PRIM/LIST/BVH/XFORM),
+                        b = phase material, f[0] = -1/density                                  */
+};
+typedef struct rt_object {
+  int32_t kind, a, b, c;
+  float f[8];
+} rt_object;
+
+enum rt_material_type {
+  RT_MAT_LAMBERTIAN = 0, RT_MAT_METAL = 1, RT_MAT_DIELECTRIC = 2,
+  RT_MAT_DIFFUSE_LIGHT = 3, RT_MAT_ISOTROPIC = 4
+};
+typedef struct rt_material {
+  int32_t type;
+  int32_t texture; /* albedo / emit texture (unused by dielectric) */
+  float param;     /* metal fuzz or dielectric index of refraction */
+  int32_t pad;
+} rt_material;
+
+enum rt_texture_type {
+  RT_TEX_SOLID = 0, RT_TEX_CHECKER = 1, RT_TEX_NOISE = 2, RT_TEX_TURBULENT = 3,
+  RT_TEX_MARBLE = 4, RT_TEX_IMAGE = 5
+};
+typedef struct rt_texture {
+  int32_t type;
+  int32_t a;       /* checker: even texture; noise/turb/marble: perlin table; image: image   */
+  int32_t b;       /* checker: odd texture; turbulent: depth                                  */
+  int32_t pad;
+  float color[3];  /* solid colour                                                            */
+  float scale;     /* noise scale                                                             */
+} rt_texture;
+
+/* Perlin tables (perlin.h:9-34). */
+typedef struct rt_perlin {
+  float ranvec[256][3];
+  int32_t perm_x[256], perm_y[256], perm_z[256];
+} rt_perlin;
+
+/* Image texture (texture.h:97-164): width, height, bytes per pixel, byte offset into texels. */
+typedef struct rt_image {
+  int32_t width, height, bytes_per_pixel;
+  int32_t offset;
+} rt_image;
+
+typedef struct rt_scene_soa {
+  rt_camera camera;
+  float background[3];
+  float aspect;
+  const int32_t* world;          int32_t n_world;   /* top-level hittable_list */
+  const rt_object* objects;      int32_t n_objects;
+  const rt_prim* prims;          int32_t n_prims;
+  const rt_triangle* triangles;  int32_t n_triangles;
+  const rt_bvh_node* nodes;      int32_t n_nodes;
+  const rt_material* materials;  int32_t n_materials;
+  const rt_texture* textures;    int32_t n_textures;
+  const rt_perlin* perlins;      int32_t n_perlins;
+  const rt_image* images;        int32_t n_images;
+  const uint8_t* texels;         int64_t n_texels;
+} rt_scene_soa;
+
+/* ------------------------------------------------------------------ render arguments */
+enum rt_cam_mode {
+  RT_CAM_REF_SLOT0 = 0, /* reference mode: lens/time draws from a private copy of
+                           the pristine slot-0 state, restarted per pixel and per fb        */
+  RT_CAM_PER_PIXEL = 1  /* lens/time draws from the pixel's own state                       */
+};
+
+typedef struct rt_render_args {
+  int32_t width, height;  /* full image size; N = width*height drives the RNG slots (H3)  */
+  int32_t spp;            /* samples_per_pixel_per_fb (render.h:24)                      */
+  int32_t fb_first;       /* first frame-buffer id `id` (render.h:154)                   */
+  int32_t fb_count;       /* number of consecutive fb ids rendered by this call          */
+  int32_t max_depth;      /* render.h:27                                                 */
+  int32_t cam_mode;       /* rt_cam_mode                                                 */
+  int32_t band_rows;      /* row tiling: rows grouped in bands of band_rows (>= 1)       */
+  int32_t band_first;     /* this call renders bands b = band_first, +band_stride, ...   */
+  int32_t band_stride;
+  int32_t stats;          /* 1: also count BVH node and primitive tests (slower)         */
+  int32_t pad;
+  uint64_t seed;          /* 1984 in the reference (render.h:91)                         */
+} rt_render_args;
+
+typedef struct rt_counters {
+  uint64_t segments;      /* top-level world->hit queries, primary + bounces (render.h:63) */
+  uint64_t node_tests;    /* stats only */
+  uint64_t prim_tests;    /* stats only */
+  uint64_t samples;
+} rt_counters;
+
+typedef struct rt_ctx rt_ctx;
+
+/* ------------------------------------------------------------------ context */
+int rt_ctx_create(int hip_device, rt_ctx** out);
+int rt_ctx_destroy(rt_ctx* ctx);
+const char* rt_last_error(const rt_ctx* ctx);
+/* Rows of the image owned by a band tiling (ascending); returns the count. rows may be NULL. */
+int32_t rt_owned_rows(const rt_render_args* a, int32_t* rows);
+
+/* Copies the flattened scene to device memory owned by the context. */
+int rt_scene_upload(rt_ctx* ctx, const rt_scene_soa* scene);
+
+/* Per-slot XORWOW states curand_init(seed, slot, 0) for slot < width*height (render.h:84-92). */
+int rt_render_init(rt_ctx* ctx, int32_t width, int32_t height, uint64_t seed);
+
+/* Renders fb ids [fb_first, fb_first+fb_count) for the owned rows into fb_dev (a DEVICE
+ * pointer): layout [fb_count][owned_rows][width][3] floats, owned rows ascending.
+ * counters may be NULL. */
+int rt_render(rt_ctx* ctx, const rt_render_args* args, float* fb_dev, rt_counters* counters);
+/* Duration in ms of the last render kernel, from HIP events recorded on the context stream. */
+float rt_last_render_ms(const rt_ctx* ctx);
+
+/* Quantise each fb (write_frame_buffer) and square-average them in fb order (average_images)
+ * for the owned rows: out_dev = DEVICE pointer, [owned_rows][width][3] bytes, owned rows
+ * ascending (row 0 of a PNG is image row height-1). */
+int rt_resolve(rt_ctx* ctx, const rt_render_args* args, const float* fb_dev, uint8_t* out_dev);
+
+/* draw(): init + render every fb + resolve, whole image, host output in PNG row order
+ * (top row first), W*H*3 bytes.  counters may be NULL. */
+int rt_draw(rt_ctx* ctx, const rt_render_args* args, uint8_t* png_rgb_host, rt_counters* counters);
+
+/* ------------------------------------------------------------------ host scene library */
+/* Builds one of the reference scenes (scenes.h) on the host: "basic", "first", "big1" (alias
+ * "random"), "two_spheres", "two_perlin", "cornell", "cornell_smoke".  The returned handle owns
+ * the arrays its rt_scene_soa points at. */
+typedef struct rt_scene_host rt_scene_host;
+int rt_scene_build(const char* name, rt_scene_host** out);
+const rt_scene_soa* rt_scene_view(const rt_scene_host* s);
+void rt_scene_free(rt_scene_host* s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_HIP_H */

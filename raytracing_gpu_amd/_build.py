@@ -1,0 +1,59 @@
+"""Build helpers: compile the gfx950 HIP library and the CPU oracle in-tree.
+
+`build_hip()` produces raytracing_gpu_amd/librt_hip.so (hipcc --offload-arch=gfx950, host + device
+code).  `build_oracle()` runs oracle/Makefile (test infrastructure only).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "librt_hip.so")
+
+HIP_SOURCES = ["rt_kernels.hip", "rt_scene.cpp"]
+HIP_DEPS = HIP_SOURCES + ["rt_detmath.h", "rt_xorwow.h"]
+# -ffp-contract=off: no FMA contraction anywhere, so every float op rounds like the reference's
+# C++ source and like the CPU oracle; fp32 div/sqrt correctly rounded (IEEE) on the device.
+HIPCC_FLAGS = [
+    "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+    "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-fast-math",
+]
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_hip(force: bool = False, verbose: bool = False) -> str:
+    deps = [os.path.join(CSRC, f) for f in HIP_DEPS] + [os.path.join(ROOT, "include", "rt_hip.h")]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, *HIPCC_FLAGS, "-o", LIB + ".tmp", *[os.path.join(CSRC, f) for f in HIP_SOURCES]]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+def build_oracle(force: bool = False) -> str:
+    odir = os.path.join(ROOT, "oracle")
+    args = ["make", "-C", odir, "-j4"]
+    if force:
+        subprocess.run(["make", "-C", odir, "clean"], check=True)
+    subprocess.run(args, check=True, stdout=subprocess.DEVNULL)
+    return os.path.join(odir, "_build", "libref_cpu.so")
+
+
+if __name__ == "__main__":
+    build_hip(force="--force" in sys.argv, verbose=True)
+    build_oracle(force="--force" in sys.argv)
+    print(LIB)

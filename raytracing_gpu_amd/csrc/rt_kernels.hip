@@ -1,0 +1,1168 @@
+// rt_kernels.hip — gfx950 render path: RNG init, the persistent path-tracing megakernel and the
+// frame-buffer resolve, plus the C ABI of include/rt_hip.h.
+//
+// Reference semantics (file:line in daRoyalCacti/Raytracing_GPU):
+//   render_init            render.h:84-92
+//   render / color_f       render.h:55-113
+//   world list             hittable_list.h:23-39
+//   BVH traversal          bvh.h:348-436      (same visiting order, stackless over the perfect tree)
+//   AABB slab test         aabb.h:19-104
+//   sphere / moving sphere sphere.h:35-73, moving_sphere.h:26-59
+//   rects / box            aarect.h:63-150, box.h:29-32
+//   translate / rotate_y   hittable.h:37-59, 112-143
+//   constant medium        constant_medium.h:34-70
+//   materials              material.h:16-138
+//   textures / perlin      texture.h:12-164, perlin.h:37-126
+//   output transform       color.h:19-170
+//
+// MI355X design: one lane owns one (frame buffer, pixel) work item and runs its samples
+// sequentially (the pixel's RNG stream is consumed in order, so samples cannot be split), but a
+// lane whose path ends starts its next sample immediately and a lane whose item ends takes a new
+// one: waves refill idle lanes from a global work counter with one atomic per refill (ballot
+// compaction), so divergent path lengths do not idle the wave.  Each loop iteration is one ray
+// segment (one world query + one scatter).  Hit records are deferred: traversal keeps only
+// (t, prim) and the winner is finalised once.  No FP contraction (-ffp-contract=off): every
+// float op rounds like the reference's C++ source.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_hip.h"
+#include "rt_detmath.h"
+#include "rt_xorwow.h"
+
+#define RT_PRIM_TYPE_MASK 0xff
+#define RT_PRIM_FLAG_UV 0x100  // material needs sphere u,v (image texture)
+
+// Scene feature mask: the render kernel is instantiated per feature set so that a scene pays
+// registers only for the primitive / object / texture kinds it contains.
+enum : int {
+  F_STATS = 1 << 0,
+  F_MOVING = 1 << 1,
+  F_RECT = 1 << 2,
+  F_TRI = 1 << 3,
+  F_LIST = 1 << 4,
+  F_XFORM = 1 << 5,
+  F_MEDIUM = 1 << 6,
+  F_CHECKER = 1 << 7,
+  F_NOISE = 1 << 8,
+  F_IMAGE = 1 << 9,
+  F_BVH = 1 << 10,
+  F_ALL = (1 << 11) - 2,
+  F_SPHERES = F_MOVING | F_CHECKER | F_BVH,  // basic, first, big1 (C2), two_spheres
+};
+
+namespace {
+
+// ------------------------------------------------------------------ device scene view
+struct DScene {
+  const int32_t* world;
+  const rt_object* objects;
+  const float4* prims;  // 3 float4 per prim: p0..p3 | p4..p7 | p8 p9 type mat
+  const rt_triangle* tris;
+  const float4* nodes;  // 2 float4 per node: lo.xyz leaf_a | hi.xyz leaf_b
+  const int4* mats;     // type, texture, param bits, pad
+  const rt_texture* texs;
+  const rt_perlin* perlins;
+  const rt_image* images;
+  const uint8_t* texels;
+  int32_t n_world;
+  int32_t pad;
+  rt_camera cam;
+  float bg[3];
+};
+
+struct V {
+  float x, y, z;
+};
+__device__ __forceinline__ V mk(float x, float y, float z) { return V{x, y, z}; }
+__device__ __forceinline__ V operator+(V a, V b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V operator-(V a, V b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V operator*(V a, V b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V operator*(float t, V v) { return mk(t * v.x, t * v.y, t * v.z); }
+__device__ __forceinline__ V neg(V a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float len2(V a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+__device__ __forceinline__ V unit(V v) { return (1.0f / __builtin_sqrtf(len2(v))) * v; }
+__device__ __forceinline__ V ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+__device__ __forceinline__ float comp(V v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+
+struct Ray {
+  V o, d;
+  float tm;
+};
+
+struct Hit {
+  V p, n;
+  float t, u, v;
+  int mat;
+  bool front;
+};
+
+__device__ __forceinline__ void set_face(Hit& h, const Ray& r, V out) {  // hittable.h:17-22
+  h.front = dot(r.d, out) < 0;
+  h.n = h.front ? out : neg(out);
+}
+
+using Rng = rtx::State;
+
+// vec3.h:129-141 (left-to-right argument order).
+__device__ __forceinline__ float urange(Rng& s, float lo, float hi) { return lo + (hi - lo) * rtx::uniform(s); }
+__device__ V in_unit_sphere(Rng& s) {
+  for (;;) {
+    const float a = urange(s, -1.0f, 1.0f);
+    const float b = urange(s, -1.0f, 1.0f);
+    const float c = urange(s, -1.0f, 1.0f);
+    const V p = mk(a, b, c);
+    if (len2(p) < 1.0f) return p;
+  }
+}
+__device__ V in_unit_disk(Rng& s) {
+  for (;;) {
+    const float a = urange(s, -1.0f, 1.0f);
+    const float b = urange(s, -1.0f, 1.0f);
+    const V p = mk(a, b, 0.0f);
+    if (len2(p) < 1.0f) return p;
+  }
+}
+
+// ------------------------------------------------------------------ primitive tests (t only)
+struct PrimRec {
+  float4 a, b, c;
+};
+__device__ __forceinline__ PrimRec load_prim(const DScene& S, int i) {
+  const float4* q = S.prims + 3 * i;
+  return PrimRec{q[0], q[1], q[2]};
+}
+__device__ __forceinline__ int prim_type(const PrimRec& q) { return __float_as_int(q.c.z) & RT_PRIM_TYPE_MASK; }
+
+__device__ __forceinline__ bool sphere_t(const Ray& r, V c, float rad, float tmin, float tmax, float& t) {
+  const V oc = r.o - c;
+  const float a = len2(r.d);
+  const float hb = dot(oc, r.d);
+  const float cc = len2(oc) - rad * rad;
+  const float disc = hb * hb - a * cc;
+  if (disc < 0) return false;
+  const float sq = __builtin_sqrtf(disc);
+  const float root = (-hb - sq) / a;  // the "second root" of sphere.h:51 is the same value (H1)
+  if (root < tmin || tmax < root) return false;
+  t = root;
+  return true;
+}
+__device__ __forceinline__ V moving_center(const PrimRec& q, float tm) {
+  return mk(q.a.x, q.a.y, q.a.z) + ((tm - q.b.w) / q.c.x) * mk(q.b.x, q.b.y, q.b.z);
+}
+// Rect axis layout: normal axis ax, in-plane axes (ia, ib).
+__device__ __forceinline__ void rect_axes(int type, int& ax, int& ia, int& ib) {
+  ax = type == RT_PRIM_RECT_XY ? 2 : (type == RT_PRIM_RECT_XZ ? 1 : 0);
+  ia = ax == 0 ? 1 : 0;
+  ib = ax == 2 ? 1 : 2;
+}
+__device__ __forceinline__ bool rect_t(const Ray& r, const PrimRec& q, int type, float tmin, float tmax, float& t) {
+  int ax, ia, ib;
+  rect_axes(type, ax, ia, ib);
+  const float tt = (q.b.x - comp(r.o, ax)) / comp(r.d, ax);
+  if (tt < tmin || tt > tmax) return false;
+  const float a = comp(r.o, ia) + tt * comp(r.d, ia);
+  const float b = comp(r.o, ib) + tt * comp(r.d, ib);
+  if (a < q.a.x || a > q.a.y || b < q.a.z || b > q.a.w) return false;
+  t = tt;
+  return true;
+}
+__device__ __forceinline__ V cross(V a, V b) {
+  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+// Moller-Trumbore, triangle.h:120-147 (bitwise | of the reference kept as a non-short-circuit or).
+__device__ __forceinline__ bool tri_t(const Ray& r, const rt_triangle& T, float tmin, float tmax, float& t, float& bu,
+                                      float& bv) {
+  const float eps = 0.0000001f;
+  const V e0 = ld3(T.e0), e1 = ld3(T.e1);
+  const V h = cross(r.d, e1);
+  const float a = dot(e0, h);
+  if (a > -eps && a < eps) return false;
+  const float f = 1.0f / a;
+  const V s = r.o - ld3(T.v0);
+  const float u = f * dot(s, h);
+  if (u < 0.0f || u > 1.0f) return false;
+  const V q = cross(s, e0);
+  const float v = f * dot(r.d, q);
+  if ((v < 0.0f) | (u + v > 1.0f)) return false;
+  const float tt = f * dot(e1, q);
+  if (tt < tmin || tt > tmax || tt < eps) return false;
+  t = tt;
+  bu = u;
+  bv = v;
+  return true;
+}
+
+template <int F>
+__device__ __forceinline__ bool prim_t(const DScene& S, int pi, const Ray& r, float tmin, float tmax, float& t,
+                                       unsigned& nprim) {
+  if constexpr ((F & F_STATS) != 0) ++nprim;
+  const PrimRec q = load_prim(S, pi);
+  const int type = prim_type(q);
+  float bu, bv;
+  if (type == RT_PRIM_SPHERE) return sphere_t(r, mk(q.a.x, q.a.y, q.a.z), q.a.w, tmin, tmax, t);
+  if constexpr ((F & F_MOVING) != 0)
+    if (type == RT_PRIM_MOVING_SPHERE) return sphere_t(r, moving_center(q, r.tm), q.a.w, tmin, tmax, t);
+  if constexpr ((F & F_TRI) != 0)
+    if (type == RT_PRIM_TRIANGLE) return tri_t(r, S.tris[(int)q.a.x], tmin, tmax, t, bu, bv);
+  if constexpr ((F & F_RECT) != 0)
+    if (type >= RT_PRIM_RECT_XY && type <= RT_PRIM_RECT_YZ) return rect_t(r, q, type, tmin, tmax, t);
+  return false;
+}
+
+// Full hit record of primitive pi at parameter t (the fields hit() sets on success).
+template <int F>
+__device__ void finalize(const DScene& S, int pi, const Ray& r, float t, Hit& h) {
+  const PrimRec q = load_prim(S, pi);
+  const int tw = __float_as_int(q.c.z);
+  const int type = tw & RT_PRIM_TYPE_MASK;
+  h.t = t;
+  h.mat = __float_as_int(q.c.w);
+  h.p = r.o + t * r.d;
+  if (type == RT_PRIM_SPHERE || type == RT_PRIM_MOVING_SPHERE) {
+    const V c = type == RT_PRIM_SPHERE ? mk(q.a.x, q.a.y, q.a.z) : moving_center(q, r.tm);
+    const V out = (1.0f / q.a.w) * (h.p - c);
+    set_face(h, r, out);
+    h.u = 0.0f;  // moving_sphere leaves u,v stale (H13): defined as 0
+    h.v = 0.0f;
+    if constexpr ((F & F_IMAGE) != 0) {
+      if (type == RT_PRIM_SPHERE && (tw & RT_PRIM_FLAG_UV)) {  // sphere.h:19-32
+        const float pi_f = 3.1415927f;
+        h.u = (rtm::det_atan2f(-out.z, out.x) + pi_f) / (2.0f * pi_f);
+        h.v = rtm::det_acosf(-out.y) / pi_f;
+      }
+    }
+    return;
+  }
+  if constexpr ((F & F_TRI) != 0) {
+   if (type == RT_PRIM_TRIANGLE) {  // triangle.h:151-175
+    const rt_triangle& T = S.tris[(int)q.a.x];
+    const V v2 = h.p - ld3(T.v0);
+    const V e0 = ld3(T.e0), e1 = ld3(T.e1);
+    const float d20 = dot(v2, e0), d21 = dot(v2, e1);
+    const float b0 = (T.d11 * d20 - T.d01 * d21) * T.inv_denom;
+    const float b1 = (T.d00 * d21 - T.d01 * d20) * T.inv_denom;
+    const float b2 = 1.0f - b0 - b1;
+    h.u = b2 * T.uv[0] + b0 * T.uv[2] + b1 * T.uv[4];
+    h.v = b2 * T.uv[1] + b0 * T.uv[3] + b1 * T.uv[5];
+    if (!T.vertex_normals) {
+      set_face(h, r, cross(e1, e0));
+    } else {
+      const V n = mk(b2 * T.n0[0] + b0 * T.n1[0] + b1 * T.n2[0], b2 * T.n0[1] + b0 * T.n1[1] + b1 * T.n2[1],
+                     b2 * T.n0[2] + b0 * T.n1[2] + b1 * T.n2[2]);
+      set_face(h, r, n);
+    }
+    return;
+   }
+  }
+  if constexpr ((F & F_RECT) != 0) {  // aarect.h
+    int ax, ia, ib;
+    rect_axes(type, ax, ia, ib);
+    const float a = comp(r.o, ia) + t * comp(r.d, ia);
+    const float b = comp(r.o, ib) + t * comp(r.d, ib);
+    h.u = (a - q.a.x) / q.b.y;
+    h.v = (b - q.a.z) / q.b.z;
+    set_face(h, r, mk(ax == 0 ? 1.0f : 0.0f, ax == 1 ? 1.0f : 0.0f, ax == 2 ? 1.0f : 0.0f));
+  }
+}
+
+// ------------------------------------------------------------------ BVH (bvh.h:348-436)
+// Kensler slab test, aabb.h:19-104, with the reciprocal hoisted per ray (same value as the
+// reference's per-node 1.0f/d).  Select-based min/max keep the reference's NaN behaviour.
+__device__ __forceinline__ bool slab(float lo, float hi, float o, float inv, float& tmin, float& tmax) {
+  float t0 = (lo - o) * inv;
+  float t1 = (hi - o) * inv;
+  if (inv < 0.0f) {
+    const float tmp = t0;
+    t0 = t1;
+    t1 = tmp;
+  }
+  tmin = t0 > tmin ? t0 : tmin;
+  tmax = t1 < tmax ? t1 : tmax;
+  return !(tmax <= tmin);
+}
+__device__ __forceinline__ bool box_hit(float4 lo, float4 hi, const Ray& r, V inv, float tmin, float tmax) {
+  if (!slab(lo.x, hi.x, r.o.x, inv.x, tmin, tmax)) return false;
+  if (!slab(lo.y, hi.y, r.o.y, inv.y, tmin, tmax)) return false;
+  return slab(lo.z, hi.z, r.o.z, inv.z, tmin, tmax);
+}
+
+// Closest primitive of a reference-layout BVH: every box is tested against the caller's
+// [tmin, tmax] (no shrinking), leaves keep strictly smaller t, visit order = depth-first,
+// left child first — identical candidate set and tie-breaking to the reference.
+template <int F>
+__device__ bool bvh_closest(const DScene& S, int base, int rows, const Ray& r, float tmin, float tmax, float& best,
+                            int& best_prim, unsigned& nnode, unsigned& nprim) {
+  const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+  const int last0 = (1 << (rows - 1)) - 1;
+  best = __builtin_inff();
+  best_prim = -1;
+  int k = 0;
+  for (;;) {
+    if constexpr ((F & F_STATS) != 0) ++nnode;
+    const float4 lo = S.nodes[2 * (base + k)];
+    const float4 hi = S.nodes[2 * (base + k) + 1];
+    bool down = false;
+    if (box_hit(lo, hi, r, inv, tmin, tmax)) {
+      if (k >= last0) {
+        float t;
+        const int pa = __float_as_int(lo.w), pb = __float_as_int(hi.w);
+        if (prim_t<F>(S, pa, r, tmin, tmax, t, nprim) && t < best) {
+          best = t;
+          best_prim = pa;
+        }
+        if (pb >= 0 && prim_t<F>(S, pb, r, tmin, tmax, t, nprim) && t < best) {
+          best = t;
+          best_prim = pb;
+        }
+      } else {
+        down = true;
+      }
+    }
+    if (down) {
+      k = 2 * k + 1;
+    } else {
+      while (k > 0 && (k & 1) == 0) k = (k - 1) >> 1;
+      if (k == 0) break;
+      k += 1;
+    }
+  }
+  return best_prim >= 0;
+}
+
+// Closest hit of a PRIM / LIST / BVH object: (t, prim).  LIST keeps the reference list rule:
+// shrinking t_max, later object wins ties (hittable_list.h:23-39).
+template <int F>
+__device__ bool leaf_closest(const DScene& S, const rt_object& o, const Ray& r, float tmin, float tmax, float& t,
+                             int& prim, unsigned& nnode, unsigned& nprim) {
+  if constexpr ((F & F_BVH) != 0)
+    if (o.kind == RT_OBJ_BVH) return bvh_closest<F>(S, o.a, o.b, r, tmin, tmax, t, prim, nnode, nprim);
+  if (o.kind == RT_OBJ_PRIM || (F & F_LIST) == 0) {
+    prim = o.a;
+    return prim_t<F>(S, o.a, r, tmin, tmax, t, nprim);
+  }
+  bool any = false;
+  float closest = tmax;
+  for (int k = 0; k < o.b; ++k) {
+    float tt;
+    if (prim_t<F>(S, o.a + k, r, tmin, closest, tt, nprim)) {
+      any = true;
+      closest = tt;
+      t = tt;
+      prim = o.a + k;
+    }
+  }
+  return any;
+}
+
+__device__ __forceinline__ Ray xform_ray(const rt_object& o, const Ray& r, Ray& moved) {
+  moved = r;
+  if (o.b & 1) moved.o = r.o - mk(o.f[0], o.f[1], o.f[2]);
+  Ray rr = moved;
+  if (o.b & 2) {
+    const float s = o.f[3], c = o.f[4];
+    rr.o.x = c * moved.o.x - s * moved.o.z;
+    rr.o.z = s * moved.o.x + c * moved.o.z;
+    rr.d.x = c * moved.d.x - s * moved.d.z;
+    rr.d.z = s * moved.d.x + c * moved.d.z;
+  }
+  return rr;
+}
+
+// t of the closest hit of an object that may be an XFORM over a leaf object.
+template <int F>
+__device__ bool xform_closest_t(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t,
+                                unsigned& nnode, unsigned& nprim) {
+  const rt_object o = S.objects[oi];
+  int prim;
+  if (o.kind != RT_OBJ_XFORM) return leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim);
+  Ray moved;
+  const Ray rr = xform_ray(o, r, moved);
+  const rt_object c = S.objects[o.a];
+  return leaf_closest<F>(S, c, rr, tmin, tmax, t, prim, nnode, nprim);
+}
+
+// hittable::hit of one top-level object with a complete record.
+template <int F>
+__device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, float tmax, Hit& h, Rng& rng,
+                           unsigned& nnode, unsigned& nprim) {
+  const rt_object o = S.objects[oi];
+  float t;
+  int prim;
+  if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {  // translate(rotate_y(child)), hittable.h:37-59, 112-143
+      Ray moved;
+      const Ray rr = xform_ray(o, r, moved);
+      const rt_object c = S.objects[o.a];
+      if (!leaf_closest<F>(S, c, rr, tmin, tmax, t, prim, nnode, nprim)) return false;
+      finalize<F>(S, prim, rr, t, h);
+      if (o.b & 2) {
+        const float s = o.f[3], cs = o.f[4];
+        const V p = mk(cs * h.p.x + s * h.p.z, h.p.y, -s * h.p.x + cs * h.p.z);
+        const V n = mk(cs * h.n.x + s * h.n.z, h.n.y, -s * h.n.x + cs * h.n.z);
+        h.p = p;
+        set_face(h, rr, n);  // rotated-frame ray against the world-frame normal (H25)
+      }
+      if (o.b & 1) {
+        h.p = h.p + mk(o.f[0], o.f[1], o.f[2]);
+        set_face(h, moved, h.n);
+      }
+      return true;
+  }
+  if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {  // constant_medium.h:34-70 (one RNG draw per qualifying query, H8)
+      const float inf = __builtin_inff();
+      float t1, t2;
+      if (!xform_closest_t<F>(S, o.a, r, -inf, inf, t1, nnode, nprim)) return false;
+      if (!xform_closest_t<F>(S, o.a, r, t1 + 0.0001f, inf, t2, nnode, nprim)) return false;
+      if (t1 < tmin) t1 = tmin;
+      if (t2 > tmax) t2 = tmax;
+      if (t1 >= t2) return false;
+      if (t1 < 0) t1 = 0;
+      const float len = __builtin_sqrtf(len2(r.d));
+      const float inside = (t2 - t1) * len;
+      const float hd = o.f[0] * rtm::det_logf(rtx::uniform(rng));
+      if (hd > inside) return false;
+      h.t = t1 + hd / len;
+      h.p = r.o + h.t * r.d;
+      h.n = mk(1.0f, 0.0f, 0.0f);
+      h.front = true;
+      h.mat = o.b;
+      h.u = 0.0f;  // stale in the reference; defined as 0
+      h.v = 0.0f;
+      return true;
+  }
+  if (!leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim)) return false;
+  finalize<F>(S, prim, r, t, h);
+  return true;
+}
+
+// World = hittable_list of top-level objects (render.h:63 with t in [0.001, inf)).
+template <int F>
+__device__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsigned& nnode, unsigned& nprim) {
+  bool any = false;
+  float closest = __builtin_inff();
+  for (int w = 0; w < S.n_world; ++w) {
+    Hit tmp;
+    if (object_hit<F>(S, S.world[w], r, 0.001f, closest, tmp, rng, nnode, nprim)) {
+      any = true;
+      closest = tmp.t;
+      h = tmp;
+    }
+  }
+  return any;
+}
+
+// ------------------------------------------------------------------ textures (texture.h, perlin.h)
+__device__ float perlin_noise(const rt_perlin& P, V p) {
+  const float u = p.x - __builtin_floorf(p.x), v = p.y - __builtin_floorf(p.y), w = p.z - __builtin_floorf(p.z);
+  const int i = (int)__builtin_floorf(p.x), j = (int)__builtin_floorf(p.y), k = (int)__builtin_floorf(p.z);
+  const float uu = u * u * (3.0f - 2.0f * u);
+  const float vv = v * v * (3.0f - 2.0f * v);
+  const float ww = w * w * (3.0f - 2.0f * w);
+  float acc = 0.0f;
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b)
+      for (int c = 0; c < 2; ++c) {
+        const int idx = P.perm_x[(i + a) & 255] ^ P.perm_y[(j + b) & 255] ^ P.perm_z[(k + c) & 255];
+        const V g = ld3(P.ranvec[idx]);
+        const V wv = mk(u - (float)a, v - (float)b, w - (float)c);
+        acc += ((float)a * uu + (float)(1 - a) * (1.0f - uu)) * ((float)b * vv + (float)(1 - b) * (1.0f - vv)) *
+               ((float)c * ww + (float)(1 - c) * (1.0f - ww)) * dot(g, wv);
+      }
+  return acc;
+}
+__device__ float perlin_turb(const rt_perlin& P, V p, int depth) {
+  double acc = 0.0, w = 1.0;
+  for (int i = 0; i < depth; ++i) {
+    acc += w * (double)perlin_noise(P, p);
+    w *= 0.5;
+    p = 2.0f * p;
+  }
+  return (float)__builtin_fabs(acc);
+}
+template <int F>
+__device__ V tex_leaf(const DScene& S, const rt_texture& T, float u, float v, V p) {
+  if constexpr ((F & F_NOISE) != 0) {
+    if (T.type == RT_TEX_NOISE) {
+      const float n = perlin_noise(S.perlins[T.a], T.scale * p);
+      return (float)(1.0 + (double)n) * (0.5f * mk(1.0f, 1.0f, 1.0f));
+    }
+    if (T.type == RT_TEX_TURBULENT) return perlin_turb(S.perlins[T.a], T.scale * p, T.b) * mk(1.0f, 1.0f, 1.0f);
+    if (T.type == RT_TEX_MARBLE) {
+      const float tb = perlin_turb(S.perlins[T.a], T.scale * p, 7);
+      const float s = 1.0f + rtm::det_sinf(T.scale * p.z + 10.0f * tb);
+      return s * (0.5f * mk(1.0f, 1.0f, 1.0f));
+    }
+  }
+  if constexpr ((F & F_IMAGE) != 0) {
+    if (T.type == RT_TEX_IMAGE) {  // texture.h:145-163
+      const rt_image im = S.images[T.a];
+      if (im.width <= 0) return mk(0.0f, 1.0f, 1.0f);
+      const float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
+      const float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+      const double vv = 1.0 - (double)vc;
+      int i = (int)(uu * (float)im.width);
+      int j = (int)(vv * (double)im.height);
+      if (i >= im.width) i = im.width - 1;
+      if (j >= im.height) j = im.height - 1;
+      const uint8_t* px =
+          S.texels + im.offset + (size_t)j * im.width * im.bytes_per_pixel + (size_t)i * im.bytes_per_pixel;
+      const float cs = 1.0f / 255.0f;
+      return mk(cs * (float)px[0], cs * (float)px[1], cs * (float)px[2]);
+    }
+  }
+  return ld3(T.color);  // solid
+}
+template <int F>
+__device__ V tex_value(const DScene& S, int ti, float u, float v, V p) {
+  const rt_texture T = S.texs[ti];
+  if constexpr ((F & F_CHECKER) != 0) {
+    if (T.type == RT_TEX_CHECKER) {  // texture.h:37-45
+      const float s = rtm::det_sinf(10.0f * p.x) * rtm::det_sinf(10.0f * p.y) * rtm::det_sinf(10.0f * p.z);
+      return tex_leaf<F>(S, S.texs[s < 0 ? T.b : T.a], u, v, p);
+    }
+  }
+  return tex_leaf<F>(S, T, u, v, p);
+}
+
+// ------------------------------------------------------------------ materials (material.h)
+// Returns true when the path continues (att, scattered set).  em = emitted colour.
+template <int F>
+__device__ bool scatter(const DScene& S, const Ray& in, const Hit& h, V& att, Ray& out, V& em, Rng& rng) {
+  const int4 m = S.mats[h.mat];
+  em = mk(0.0f, 0.0f, 0.0f);
+  switch (m.x) {
+    case RT_MAT_LAMBERTIAN: {
+      V dir = h.n + unit(in_unit_sphere(rng));
+      const float e = 1e-6f;
+      if (__builtin_fabsf(dir.x) < e && __builtin_fabsf(dir.y) < e && __builtin_fabsf(dir.z) < e) dir = h.n;
+      out = Ray{h.p, dir, in.tm};
+      att = tex_value<F>(S, m.y, h.u, h.v, h.p);
+      return true;
+    }
+    case RT_MAT_METAL: {
+      const V ud = unit(in.d);
+      const V refl = ud - (2.0f * dot(ud, h.n)) * h.n;
+      const float fuzz = __int_as_float(m.z);
+      out = Ray{h.p, refl + fuzz * in_unit_sphere(rng), in.tm};
+      att = tex_value<F>(S, m.y, h.u, h.v, h.p);
+      return dot(out.d, h.n) > 0;
+    }
+    case RT_MAT_DIELECTRIC: {
+      att = mk(1.0f, 1.0f, 1.0f);
+      const float ir = __int_as_float(m.z);
+      const float ratio = h.front ? (1.0f / ir) : ir;
+      const V ud = unit(in.d);
+      const float c = __builtin_fminf(dot(neg(ud), h.n), 1.0f);
+      const float sn = __builtin_sqrtf(1.0f - c * c);
+      V dir;
+      bool refl = ratio * sn > 1.0f;
+      if (!refl) {
+        const float sr = (1.0f - ratio) / (1.0f + ratio);
+        const float r0 = sr * sr;
+        const float rf = r0 + (1.0f - r0) * rtm::det_pow5f(1.0f - c);
+        refl = rf > rtx::uniform(rng);
+      }
+      if (refl) {
+        dir = ud - (2.0f * dot(ud, h.n)) * h.n;
+      } else {  // vec3.h:152-158
+        const float ct = __builtin_fminf(dot(neg(ud), h.n), 1.0f);
+        const V perp = ratio * (ud + ct * h.n);
+        const V par = (-__builtin_sqrtf(__builtin_fabsf(1.0f - len2(perp)))) * h.n;
+        dir = perp + par;
+      }
+      out = Ray{h.p, dir, in.tm};
+      return true;
+    }
+    case RT_MAT_DIFFUSE_LIGHT:
+      em = tex_value<F>(S, m.y, h.u, h.v, h.p);
+      return false;
+    default: {  // isotropic
+      out = Ray{h.p, in_unit_sphere(rng), in.tm};
+      att = tex_value<F>(S, m.y, h.u, h.v, h.p);
+      return true;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ kernels
+struct RenderParams {
+  DScene S;
+  const uint4* states;  // 2 uint4 per slot: d v0 v1 v2 | v3 v4 - -
+  float* fb;
+  const int32_t* row_map;
+  unsigned long long* work;
+  unsigned long long* counters;  // segments, node, prim, samples
+  unsigned long long total_items;
+  long long npix;  // W*H of the full image
+  int W, H, rows, spp, fb_first, max_depth, cam_mode, pad;
+  uint32_t cam_state[6];
+};
+
+constexpr int kBlock = 256;
+constexpr int kRefill = 16;  // refill a wave once this many lanes are idle
+
+__device__ __forceinline__ unsigned lane_rank(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+
+template <int F>
+__global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
+  const DScene& S = P.S;
+  const unsigned lane = __lane_id();
+  long long item = -1;  // -1: idle
+  bool done = false;
+  int f = 0, i = 0, r = 0, j = 0, s = 0, depth = 0;
+  Rng loc{}, cam{};
+  Ray ray{};
+  V att = mk(1, 1, 1), col = mk(0, 0, 0);
+  unsigned long long nseg = 0, nsamp = 0;
+  unsigned nnode = 0, nprim = 0;
+  const bool per_pixel = P.cam_mode == RT_CAM_PER_PIXEL;
+  const rt_camera& C = S.cam;
+
+  for (;;) {
+    // ---- refill idle lanes (one atomic per wave, ballot-compacted ranks)
+    const unsigned long long idle = __ballot(item < 0 && !done);
+    const unsigned long long busy = __ballot(item >= 0);
+    const int nidle = __popcll(idle);
+    if (nidle > 0 && (nidle >= kRefill || busy == 0)) {
+      const int leader = __ffsll((long long)idle) - 1;
+      unsigned long long base = 0;
+      if ((int)lane == leader) base = atomicAdd(P.work, (unsigned long long)nidle);
+      base = __shfl(base, leader, 64);
+      if (item < 0 && !done) {
+        const unsigned long long mine = base + lane_rank(idle);
+        if (mine >= P.total_items) {
+          done = true;
+        } else {
+          item = (long long)mine;
+          const long long per_fb = (long long)P.rows * P.W;
+          f = (int)(item / per_fb);
+          const long long rem = item - (long long)f * per_fb;
+          r = (int)(rem / P.W);
+          i = (int)(rem - (long long)r * P.W);
+          j = P.row_map[r];
+          const long long id = P.fb_first + f;
+          const long long p = (long long)j * P.W + i;
+          const long long slot = ((id + 1) * p + id + 1) % P.npix;  // render.h:101 (H3)
+          const uint4 s0 = P.states[2 * slot], s1 = P.states[2 * slot + 1];
+          loc.d = s0.x; loc.v[0] = s0.y; loc.v[1] = s0.z; loc.v[2] = s0.w; loc.v[3] = s1.x; loc.v[4] = s1.y;
+          s = 0;
+          depth = 0;
+          col = mk(0, 0, 0);
+        }
+      }
+    }
+    if (__ballot(item >= 0) == 0) break;
+    if (item < 0) continue;
+
+    // ---- begin a sample: jitter + camera ray (render.h:105-108, camera.h:49-58)
+    if (depth == 0) {
+      if (s == 0) {
+        cam.d = P.cam_state[0];
+        for (int k = 0; k < 5; ++k) cam.v[k] = P.cam_state[1 + k];
+      }
+      const float u = ((float)i + rtx::uniform(loc)) / (float)P.W;
+      const float v = ((float)j + rtx::uniform(loc)) / (float)P.H;
+      Rng& cr = per_pixel ? loc : cam;
+      const V rd = C.lens_radius * in_unit_disk(cr);
+      const V off = rd.x * ld3(C.u) + rd.y * ld3(C.v);
+      ray.o = ld3(C.origin) + off;
+      ray.d = ld3(C.lower_left) + u * ld3(C.horizontal) + v * ld3(C.vertical) - ld3(C.origin) - off;
+      ray.tm = urange(cr, C.time0, C.time1);
+      att = mk(1.0f, 1.0f, 1.0f);
+    }
+
+    // ---- one segment (render.h:60-77)
+    ++nseg;
+    Hit h;
+    bool ended = false;
+    V contrib;
+    if (!world_hit<F>(S, ray, h, loc, nnode, nprim)) {
+      contrib = att * ld3(S.bg);
+      ended = true;
+    } else {
+      V a, em;
+      Ray sc;
+      if (scatter<F>(S, ray, h, a, sc, em, loc)) {
+        att = att * a;
+        ray = sc;
+        if (++depth == P.max_depth) {
+          contrib = mk(0.0f, 0.0f, 0.0f);
+          ended = true;
+        }
+      } else {
+        contrib = att * em;
+        ended = true;
+      }
+    }
+    if (ended) {
+      col = col + contrib;
+      depth = 0;
+      ++nsamp;
+      if (++s == P.spp) {
+        const V out = (1.0f / (float)P.spp) * col;
+        float* dst = P.fb + 3 * (((long long)f * P.rows + r) * P.W + i);
+        dst[0] = out.x;
+        dst[1] = out.y;
+        dst[2] = out.z;
+        item = -1;
+      }
+    }
+  }
+
+  const unsigned long long ws = wave_sum(nseg), wm = wave_sum(nsamp);
+  unsigned long long wn = 0, wp = 0;
+  if constexpr ((F & F_STATS) != 0) {
+    wn = wave_sum(nnode);
+    wp = wave_sum(nprim);
+  }
+  if (lane == 0) {
+    atomicAdd(&P.counters[0], ws);
+    atomicAdd(&P.counters[3], wm);
+    if constexpr ((F & F_STATS) != 0) {
+      atomicAdd(&P.counters[1], wn);
+      atomicAdd(&P.counters[2], wp);
+    }
+  }
+}
+
+// curand_init(seed, slot, 0) for every slot < n (render.h:84-92): seed scramble, then the
+// subsequence jump A^(slot * 2^67) applied digit by digit in base 4 (as skipahead_sequence).
+// The jump matrix of each digit position is wave-uniform; lanes mask the applications.
+__global__ __launch_bounds__(kBlock) void init_states_kernel(uint4* states, long long n, uint64_t seed,
+                                                            const uint32_t* __restrict__ seq, int digits) {
+  const long long slot = (long long)blockIdx.x * kBlock + threadIdx.x;
+  const bool live = slot < n;
+  rtx::State st = rtx::seed_state(seed);
+  unsigned long long x = live ? (unsigned long long)slot : 0ull;
+  for (int d = 0; d < digits; ++d) {
+    const unsigned dig = (unsigned)(x & 3u);
+    x >>= 2;
+    const uint32_t* m = seq + 800 * d;
+    for (unsigned t = 0; t < 3; ++t) {
+      if (t < dig) {
+        uint32_t out[5];
+        rtx::mat_apply(m, st.v, out);
+        for (int k = 0; k < 5; ++k) st.v[k] = out[k];
+      }
+    }
+  }
+  if (live) {
+    states[2 * slot] = make_uint4(st.d, st.v[0], st.v[1], st.v[2]);
+    states[2 * slot + 1] = make_uint4(st.v[3], st.v[4], 0u, 0u);
+  }
+}
+
+// write_frame_buffer quantisation (color.h:40-44); NaN defined as 0.
+__device__ __forceinline__ int quant(float x) {
+  const float r = __builtin_sqrtf(x);
+  if (!(r == r)) return 0;
+  const float c = r < 0.0f ? 0.0f : (r > 0.999f ? 0.999f : r);
+  return (int)(256.0f * c);
+}
+
+// average_images (color.h:57-170) over fbs 0..nfb-1 in order, per owned pixel.
+__global__ __launch_bounds__(kBlock) void resolve_kernel(const float* __restrict__ fb, uint8_t* __restrict__ out,
+                                                        long long per_fb, int nfb) {
+  const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= per_fb) return;
+  float acc = 0.0f;
+  for (int f = 0; f < nfb; ++f) {
+    const int c = quant(fb[(long long)f * per_fb + k]);
+    acc += (float)(c * c) / (255.0f * 255.0f);
+  }
+  out[k] = (uint8_t)quant(acc / (float)nfb);
+}
+
+}  // namespace
+
+// ====================================================================== host side (C ABI)
+struct rt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::string err;
+  std::vector<void*> scene_bufs;
+  DScene scene{};
+  bool have_scene = false;
+  uint4* states = nullptr;
+  long long states_n = 0;
+  uint64_t states_seed = 0;
+  uint32_t* seq = nullptr;
+  unsigned long long* work = nullptr;  // [0] work counter, [1..4] counters
+  int32_t* row_map = nullptr;
+  int row_cap = 0;
+  int cus = 0, blocks_per_cu[8] = {0};
+  int features = 0;
+  float last_ms = 0.0f;
+};
+
+namespace {
+
+struct Variant {
+  int mask;
+  const void* fn;
+};
+const Variant kVariants[] = {
+    {F_SPHERES, (const void*)render_kernel<F_SPHERES>},
+    {F_ALL, (const void*)render_kernel<F_ALL>},
+    {F_SPHERES | F_STATS, (const void*)render_kernel<F_SPHERES | F_STATS>},
+    {F_ALL | F_STATS, (const void*)render_kernel<F_ALL | F_STATS>},
+};
+constexpr int kNumVariants = 4;
+
+// Smallest compiled variant that covers the scene's features.
+int pick_variant(int features, bool stats) {
+  for (int v = 0; v < kNumVariants; ++v) {
+    const int m = kVariants[v].mask;
+    if (((m & F_STATS) != 0) == stats && (features & ~m & ~F_STATS) == 0) return v;
+  }
+  return stats ? 3 : 1;
+}
+
+int scene_features(const rt_scene_soa* s) {
+  int f = 0;
+  for (int k = 0; k < s->n_prims; ++k) {
+    const int t = s->prims[k].type;
+    if (t == RT_PRIM_MOVING_SPHERE) f |= F_MOVING;
+    if (t >= RT_PRIM_RECT_XY && t <= RT_PRIM_RECT_YZ) f |= F_RECT;
+    if (t == RT_PRIM_TRIANGLE) f |= F_TRI;
+  }
+  for (int k = 0; k < s->n_objects; ++k) {
+    const int t = s->objects[k].kind;
+    if (t == RT_OBJ_LIST) f |= F_LIST;
+    if (t == RT_OBJ_BVH) f |= F_BVH;
+    if (t == RT_OBJ_XFORM) f |= F_XFORM;
+    if (t == RT_OBJ_MEDIUM) f |= F_MEDIUM;
+  }
+  for (int k = 0; k < s->n_textures; ++k) {
+    const int t = s->textures[k].type;
+    if (t == RT_TEX_CHECKER) f |= F_CHECKER;
+    if (t == RT_TEX_NOISE || t == RT_TEX_TURBULENT || t == RT_TEX_MARBLE) f |= F_NOISE;
+    if (t == RT_TEX_IMAGE) f |= F_IMAGE;
+  }
+  return f;
+}
+
+int fail(rt_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+#define HIPCHK(ctx, call)                                                                          \
+  do {                                                                                             \
+    hipError_t e_ = (call);                                                                        \
+    if (e_ != hipSuccess) return fail(ctx, RT_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+int upload(rt_ctx* c, const T* src, size_t n, const T** dst) {
+  *dst = nullptr;
+  if (n == 0) return RT_OK;
+  void* p = nullptr;
+  HIPCHK(c, hipMalloc(&p, n * sizeof(T)));
+  c->scene_bufs.push_back(p);
+  HIPCHK(c, hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice));
+  *dst = (const T*)p;
+  return RT_OK;
+}
+
+void free_scene(rt_ctx* c) {
+  for (void* p : c->scene_bufs) (void)hipFree(p);
+  c->scene_bufs.clear();
+  c->have_scene = false;
+}
+
+bool tex_needs_uv(const rt_scene_soa* s, int ti) {
+  if (ti < 0 || ti >= s->n_textures) return false;
+  const rt_texture& t = s->textures[ti];
+  if (t.type == RT_TEX_IMAGE) return true;
+  if (t.type == RT_TEX_CHECKER) {
+    for (int c : {t.a, t.b})
+      if (c >= 0 && c < s->n_textures && s->textures[c].type == RT_TEX_IMAGE) return true;
+  }
+  return false;
+}
+
+int validate_args(rt_ctx* c, const rt_render_args* a) {
+  if (!a) return fail(c, RT_ERR_ARG, "null args");
+  if (a->width <= 0 || a->height <= 0 || a->spp <= 0 || a->fb_count <= 0 || a->fb_first < 0 || a->max_depth <= 0)
+    return fail(c, RT_ERR_ARG, "bad render args");
+  if (a->band_rows <= 0 || a->band_stride <= 0 || a->band_first < 0 || a->band_first >= a->band_stride)
+    return fail(c, RT_ERR_ARG, "bad band tiling");
+  if (a->cam_mode != RT_CAM_REF_SLOT0 && a->cam_mode != RT_CAM_PER_PIXEL) return fail(c, RT_ERR_ARG, "bad cam_mode");
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_ctx_create(int hip_device, rt_ctx** out) {
+  if (!out) return RT_ERR_ARG;
+  *out = nullptr;
+  rt_ctx* c = new rt_ctx;
+  c->device = hip_device;
+  int rc = RT_OK;
+  auto chk = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && rc == RT_OK) rc = fail(c, RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  };
+  chk(hipSetDevice(hip_device), "hipSetDevice");
+  if (rc == RT_OK) chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+  if (rc == RT_OK) chk(hipEventCreate(&c->ev0), "hipEventCreate");
+  if (rc == RT_OK) chk(hipEventCreate(&c->ev1), "hipEventCreate");
+  if (rc == RT_OK) chk(hipMalloc((void**)&c->work, 8 * sizeof(unsigned long long)), "hipMalloc");
+  if (rc == RT_OK) {
+    std::vector<uint32_t> seq(32 * 800);
+    rtx::build_sequence_jumps(seq.data());
+    chk(hipMalloc((void**)&c->seq, seq.size() * 4), "hipMalloc");
+    if (rc == RT_OK) chk(hipMemcpy(c->seq, seq.data(), seq.size() * 4, hipMemcpyHostToDevice), "hipMemcpy");
+  }
+  if (rc == RT_OK) {
+    hipDeviceProp_t prop;
+    chk(hipGetDeviceProperties(&prop, hip_device), "hipGetDeviceProperties");
+    c->cus = prop.multiProcessorCount;
+    for (int v = 0; v < kNumVariants; ++v)
+      chk(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->blocks_per_cu[v], kVariants[v].fn, kBlock, 0),
+          "occupancy");
+  }
+  if (rc != RT_OK) {
+    fprintf(stderr, "rt_ctx_create: %s\n", c->err.c_str());
+    rt_ctx_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return RT_OK;
+}
+
+int rt_ctx_destroy(rt_ctx* c) {
+  if (!c) return RT_OK;
+  (void)hipSetDevice(c->device);
+  free_scene(c);
+  if (c->states) (void)hipFree(c->states);
+  if (c->seq) (void)hipFree(c->seq);
+  if (c->work) (void)hipFree(c->work);
+  if (c->row_map) (void)hipFree(c->row_map);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return RT_OK;
+}
+
+const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int32_t rt_owned_rows(const rt_render_args* a, int32_t* rows) {
+  if (!a || a->band_rows <= 0 || a->band_stride <= 0) return 0;
+  int32_t n = 0;
+  for (int32_t b = a->band_first; (int64_t)b * a->band_rows < a->height; b += a->band_stride)
+    for (int32_t j = b * a->band_rows; j < (b + 1) * a->band_rows && j < a->height; ++j) {
+      if (rows) rows[n] = j;
+      ++n;
+    }
+  return n;
+}
+
+int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
+  if (!c || !s) return RT_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (s->n_world <= 0 || !s->world || s->n_objects <= 0 || s->n_materials <= 0)
+    return fail(c, RT_ERR_SCENE, "empty scene");
+  for (int k = 0; k < s->n_world; ++k)
+    if (s->world[k] < 0 || s->world[k] >= s->n_objects) return fail(c, RT_ERR_SCENE, "world index out of range");
+  for (int k = 0; k < s->n_objects; ++k) {
+    const rt_object& o = s->objects[k];
+    if (o.kind == RT_OBJ_BVH && (o.b < 2 || o.a < 0 || o.a + (1 << o.b) - 1 > s->n_nodes))
+      return fail(c, RT_ERR_SCENE, "bvh out of range");
+    if ((o.kind == RT_OBJ_PRIM || o.kind == RT_OBJ_LIST) && (o.a < 0 || o.a + (o.kind == RT_OBJ_LIST ? o.b : 1) > s->n_prims))
+      return fail(c, RT_ERR_SCENE, "prim index out of range");
+    if ((o.kind == RT_OBJ_XFORM || o.kind == RT_OBJ_MEDIUM) && (o.a < 0 || o.a >= s->n_objects))
+      return fail(c, RT_ERR_SCENE, "child object out of range");
+  }
+  for (int k = 0; k < s->n_prims; ++k)
+    if (s->prims[k].material < 0 || s->prims[k].material >= s->n_materials)
+      return fail(c, RT_ERR_SCENE, "prim material out of range");
+  free_scene(c);
+  // Device copy of the primitives with the u,v flag folded into the type word.
+  std::vector<rt_prim> prims(s->prims, s->prims + s->n_prims);
+  for (rt_prim& p : prims) {
+    const rt_material& m = s->materials[p.material];
+    if (p.type == RT_PRIM_SPHERE && m.type != RT_MAT_DIELECTRIC && tex_needs_uv(s, m.texture)) p.type |= RT_PRIM_FLAG_UV;
+  }
+  DScene& d = c->scene;
+  d = DScene{};
+  const rt_prim* dp;
+  const rt_bvh_node* dn;
+  const rt_material* dm;
+  int rc;
+  if ((rc = upload(c, s->world, (size_t)s->n_world, &d.world))) return rc;
+  if ((rc = upload(c, s->objects, (size_t)s->n_objects, &d.objects))) return rc;
+  if ((rc = upload(c, prims.data(), prims.size(), &dp))) return rc;
+  if ((rc = upload(c, s->triangles, (size_t)s->n_triangles, &d.tris))) return rc;
+  if ((rc = upload(c, s->nodes, (size_t)s->n_nodes, &dn))) return rc;
+  if ((rc = upload(c, s->materials, (size_t)s->n_materials, &dm))) return rc;
+  if ((rc = upload(c, s->textures, (size_t)s->n_textures, &d.texs))) return rc;
+  if ((rc = upload(c, s->perlins, (size_t)s->n_perlins, &d.perlins))) return rc;
+  if ((rc = upload(c, s->images, (size_t)s->n_images, &d.images))) return rc;
+  if ((rc = upload(c, s->texels, (size_t)s->n_texels, &d.texels))) return rc;
+  d.prims = (const float4*)dp;
+  d.nodes = (const float4*)dn;
+  d.mats = (const int4*)dm;
+  d.n_world = s->n_world;
+  d.cam = s->camera;
+  d.bg[0] = s->background[0];
+  d.bg[1] = s->background[1];
+  d.bg[2] = s->background[2];
+  c->features = scene_features(s);
+  c->have_scene = true;
+  return RT_OK;
+}
+
+int rt_render_init(rt_ctx* c, int32_t width, int32_t height, uint64_t seed) {
+  if (!c || width <= 0 || height <= 0) return fail(c, RT_ERR_ARG, "bad init args");
+  HIPCHK(c, hipSetDevice(c->device));
+  const long long n = (long long)width * height;
+  if (n != c->states_n) {
+    if (c->states) HIPCHK(c, hipFree(c->states));
+    c->states = nullptr;
+    c->states_n = 0;
+    HIPCHK(c, hipMalloc((void**)&c->states, (size_t)n * 2 * sizeof(uint4)));
+    c->states_n = n;
+  }
+  int digits = 0;
+  for (unsigned long long x = (unsigned long long)(n - 1); x; x >>= 2) ++digits;
+  const long long blocks = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(init_states_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, c->states, n, seed,
+                     (const uint32_t*)c->seq, digits);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->states_seed = seed;
+  return RT_OK;
+}
+
+int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* counters) {
+  if (!c) return RT_ERR_ARG;
+  int rc = validate_args(c, a);
+  if (rc) return rc;
+  if (!c->have_scene) return fail(c, RT_ERR_STATE, "no scene uploaded");
+  if (!c->states || c->states_n != (long long)a->width * a->height || c->states_seed != a->seed)
+    return fail(c, RT_ERR_STATE, "rt_render_init not called for this size/seed");
+  if (!fb_dev) return fail(c, RT_ERR_ARG, "null fb");
+  HIPCHK(c, hipSetDevice(c->device));
+  const int rows = rt_owned_rows(a, nullptr);
+  if (rows <= 0) return fail(c, RT_ERR_ARG, "no rows owned");
+  if (rows > c->row_cap) {
+    if (c->row_map) HIPCHK(c, hipFree(c->row_map));
+    c->row_map = nullptr;
+    HIPCHK(c, hipMalloc((void**)&c->row_map, rows * sizeof(int32_t)));
+    c->row_cap = rows;
+  }
+  std::vector<int32_t> rm(rows);
+  rt_owned_rows(a, rm.data());
+  HIPCHK(c, hipMemcpyAsync(c->row_map, rm.data(), rows * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->work, 0, 8 * sizeof(unsigned long long), c->stream));
+
+  RenderParams P{};
+  P.S = c->scene;
+  P.states = c->states;
+  P.fb = fb_dev;
+  P.row_map = c->row_map;
+  P.work = c->work;
+  P.counters = c->work + 1;
+  P.total_items = (unsigned long long)a->fb_count * rows * a->width;
+  P.npix = (long long)a->width * a->height;
+  P.W = a->width;
+  P.H = a->height;
+  P.rows = rows;
+  P.spp = a->spp;
+  P.fb_first = a->fb_first;
+  P.max_depth = a->max_depth;
+  P.cam_mode = a->cam_mode;
+  const rtx::State cs = rtx::seed_state(a->seed);  // pristine slot 0 = curand_init(seed, 0, 0)
+  P.cam_state[0] = cs.d;
+  for (int k = 0; k < 5; ++k) P.cam_state[1 + k] = cs.v[k];
+
+  const bool stats = a->stats != 0;
+  const int var = pick_variant(c->features, stats);
+  const long long resident = (long long)c->cus * std::max(1, c->blocks_per_cu[var]);
+  const long long need = (long long)((P.total_items + kBlock - 1) / kBlock);
+  const unsigned blocks = (unsigned)std::max(1LL, std::min(resident, need));
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  void* kargs[] = {&P};
+  HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(kBlock), kargs, 0, c->stream));
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  unsigned long long host_cnt[8];
+  HIPCHK(c, hipMemcpyAsync(host_cnt, c->work, sizeof(host_cnt), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+  if (counters) {
+    counters->segments = host_cnt[1];
+    counters->node_tests = host_cnt[2];
+    counters->prim_tests = host_cnt[3];
+    counters->samples = host_cnt[4];
+  }
+  if (host_cnt[4] != (unsigned long long)a->spp * P.total_items)
+    return fail(c, RT_ERR_HIP, "render kernel did not complete every sample");
+  return RT_OK;
+}
+
+float rt_last_render_ms(const rt_ctx* c) { return c ? c->last_ms : 0.0f; }
+
+int rt_resolve(rt_ctx* c, const rt_render_args* a, const float* fb_dev, uint8_t* out_dev) {
+  if (!c) return RT_ERR_ARG;
+  int rc = validate_args(c, a);
+  if (rc) return rc;
+  if (!fb_dev || !out_dev) return fail(c, RT_ERR_ARG, "null buffer");
+  HIPCHK(c, hipSetDevice(c->device));
+  const long long per_fb = (long long)rt_owned_rows(a, nullptr) * a->width * 3;
+  const long long blocks = (per_fb + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, fb_dev, out_dev, per_fb,
+                     a->fb_count);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return RT_OK;
+}
+
+int rt_draw(rt_ctx* c, const rt_render_args* a, uint8_t* png_rgb_host, rt_counters* counters) {
+  if (!c || !png_rgb_host) return RT_ERR_ARG;
+  rt_render_args full = *a;
+  full.band_rows = a->height;
+  full.band_first = 0;
+  full.band_stride = 1;
+  int rc = validate_args(c, &full);
+  if (rc) return rc;
+  if ((rc = rt_render_init(c, a->width, a->height, a->seed))) return rc;
+  const size_t npx = (size_t)a->width * a->height;
+  float* fb = nullptr;
+  uint8_t* img = nullptr;
+  HIPCHK(c, hipMalloc((void**)&fb, npx * 3 * sizeof(float) * a->fb_count));
+  if (hipMalloc((void**)&img, npx * 3) != hipSuccess) {
+    (void)hipFree(fb);
+    return fail(c, RT_ERR_NOMEM, "hipMalloc image");
+  }
+  rc = rt_render(c, &full, fb, counters);
+  if (!rc) rc = rt_resolve(c, &full, fb, img);
+  std::vector<uint8_t> tmp(npx * 3);
+  if (!rc && hipMemcpy(tmp.data(), img, tmp.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(c, RT_ERR_HIP, "copy image");
+  (void)hipFree(fb);
+  (void)hipFree(img);
+  if (rc) return rc;
+  const size_t row = (size_t)a->width * 3;
+  for (int j = 0; j < a->height; ++j) memcpy(png_rgb_host + (size_t)(a->height - 1 - j) * row, tmp.data() + j * row, row);
+  return RT_OK;
+}
+
+}  // extern "C"
