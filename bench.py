@@ -182,14 +182,10 @@ def main():
             out["cpu_baseline"] = cpu_baseline(a, a.cpu_seconds)
         print(json.dumps(out), flush=True)
         if a.png:
-            import numpy as np
+            from raytracing_gpu_amd import dist as rdist
 
             g = (gathered if world > 1 else img).cpu().numpy().reshape(world, max_rows, a.width, 3)
-            pic = np.zeros((a.height, a.width, 3), np.uint8)
-            for r in range(world):
-                for k, j in enumerate(all_rows[r]):
-                    pic[a.height - 1 - j] = g[r, k]
-            rt.write_png(a.png, pic)
+            rt.write_png(a.png, rdist.assemble(g, all_rows, a.height))
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -119,6 +119,12 @@ def lib() -> ctypes.CDLL:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} missing: run `python -m raytracing_gpu_amd._build` "
                                "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        # torch (device memory, streams, RCCL) bundles its own libamdhip64.so.7: load it first so
+        # this library binds to the same HIP runtime instance instead of a second copy.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in ABI.items():
             fn = getattr(L, name)

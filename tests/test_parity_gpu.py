@@ -124,3 +124,24 @@ def test_stats_counters_match_oracle(rtlib, gpu_ctx, oracle):
     assert cnt["segments"] == c["segments"]
     assert cnt["node_tests"] == c["node_tests"]
     assert cnt["prim_tests"] == c["prim_tests"]
+
+
+@pytest.mark.parametrize("key,scene,W,H,spp,fbs,depth", [
+    ("c1_basic", "basic", 200, 100, 1, [0], 1),
+    ("c2_big1", "big1", 120, 68, 4, [0, 1], 50),
+    ("c3_cornell_smoke", "cornell_smoke", 64, 64, 4, [0, 1], 50),
+])
+def test_against_committed_golden(rtlib, gpu_ctx, key, scene, W, H, spp, fbs, depth):
+    """GPU output vs the committed oracle fixtures (tests/golden/renders.npz), without the live oracle."""
+    import os
+
+    import torch
+
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "renders.npz"))
+    gpu, _, cnt, args, fb = _gpu_render(rtlib, gpu_ctx, scene, W, H, spp, fbs[0], len(fbs), REF, depth=depth)
+    for k, f in enumerate(fbs):
+        assert np.array_equal(_bits(gpu[k]), _bits(g[f"{key}_fb{f}"]))
+    assert cnt["segments"] == sum(int(g[f"{key}_fb{f}_segments"][0]) for f in fbs)
+    out = torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda")
+    gpu_ctx.resolve(args, fb.data_ptr(), out.data_ptr())
+    assert np.array_equal(out.cpu().numpy().reshape(H, W, 3)[::-1], g[f"{key}_png"])
