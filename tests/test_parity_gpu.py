@@ -77,8 +77,9 @@ def test_resolve_matches_average_images(rtlib, gpu_ctx, oracle):
 def test_draw_entry_point(rtlib, gpu_ctx, oracle):
     s = rtlib.render_settings(image_width=80, samples_per_pixel_per_fb=2, no_fb=2, max_depth=50)
     img, cnt = rtlib.draw(rtlib.Scene.builtin("basic"), s, ctx=gpu_ctx)
-    assert img.shape == (s.image_height, 80, 3) and s.image_height == 45  # int(80/(16/9)) (H18)
-    want, _, tot = oracle.draw("basic", 80, 45, 2, 2)
+    # int(80 / double(16.0f/9.0f)) = int(44.9999993) = 44 (H18)
+    assert img.shape == (s.image_height, 80, 3) and s.image_height == 44
+    want, _, tot = oracle.draw("basic", 80, 44, 2, 2)
     assert np.array_equal(img, want)
     assert cnt["segments"] == tot["segments"]
 
