@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--cam", choices=["ref", "per_pixel"], default="ref")
     ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--exact", action="store_true", help="reference BVH visit set (no culling)")
+    ap.add_argument("--no-lds", action="store_true", help="keep the scene in global memory")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the untimed node/prim counting pass")
@@ -97,7 +99,7 @@ def main():
     ctx.upload(sc)
     cam = rt.RT_CAM_REF_SLOT0 if a.cam == "ref" else rt.RT_CAM_PER_PIXEL
     args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, band_rows=a.band_rows,
-                        band_first=rank, band_stride=world)
+                        band_first=rank, band_stride=world, exact=a.exact, lds=not a.no_lds)
     rows = rt.owned_rows(args)
     all_rows = []
     for r in range(world):
@@ -113,7 +115,7 @@ def main():
     if not a.no_stats:  # untimed pass of the counting variant: node / prim tests for B_seg
         ctx.render_init(a.width, a.height, 1984)
         sargs = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, band_rows=a.band_rows,
-                             band_first=rank, band_stride=world, stats=True)
+                             band_first=rank, band_stride=world, stats=True, exact=a.exact)
         stats = ctx.render(sargs, fb.data_ptr())
 
     seg_step = [0]
@@ -165,14 +167,16 @@ def main():
                     "bytes_per_launch": int(bytes_launch),
                     "bytes_per_segment": round(bytes_launch / max(stats["segments"], 1), 2),
                     "node_tests_per_segment": round(stats["node_tests"] / max(stats["segments"], 1), 3),
-                    "prim_tests_per_segment": round(stats["prim_tests"] / max(stats["segments"], 1), 3)}
+                    "prim_tests_per_segment": round(stats["prim_tests"] / max(stats["segments"], 1), 3),
+                    "fallbacks": stats["fallbacks"]}
         out = {
             "metric": "Mrays/sec (primary+bounces) on RTIOW random-spheres 1200x800x100spp",
             "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (reference scene generator, seed 1984)",
             "config": {"workload": f"C2 {a.scene} {a.width}x{a.height}, {a.nfb} fb x {a.spp} spp = "
-                                   f"{a.nfb * a.spp} rays/pixel, depth {a.depth}, cam {a.cam}",
+                                   f"{a.nfb * a.spp} rays/pixel, depth {a.depth}, cam {a.cam}, "
+                                   f"traversal {'exact' if a.exact else 'culled'}",
                        "scene": a.scene, "width": a.width, "height": a.height, "rays_per_pixel": a.nfb * a.spp,
                        "no_fb": a.nfb, "spp_per_fb": a.spp, "max_depth": a.depth,
                        "segments_per_step": int(segs), "parallelism": f"rows{world}"},

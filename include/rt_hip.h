@@ -64,19 +64,21 @@ typedef struct rt_prim {
   int32_t material;
 } rt_prim;
 
-/* Triangle (triangle.h:19-41 constructor output), 128 bytes. */
+/* Triangle (triangle.h:19-41 constructor output), 144 bytes. */
 typedef struct rt_triangle {
-  float v0[3], e0[3], e1[3]; /* vertex0, vertex1-vertex0, vertex2-vertex0 */
+  float v0[3], v1[3], v2[3];
+  float e0[3], e1[3];        /* vertex1-vertex0, vertex2-vertex0 (triangle.h:26-27) */
   float d00, d01, d11, inv_denom;
   float uv[6];               /* u0 v0 u1 v1 u2 v2 */
   float n0[3], n1[3], n2[3];
   int32_t vertex_normals;
-  int32_t pad[2];
+  int32_t pad;
 } rt_triangle;
 
 /* Inner node of a reference-layout BVH (bvh.h:133-346): a perfect binary tree of `rows` inner
  * levels stored in heap order (children of k are 2k+1, 2k+2).  Nodes of the last inner level
- * carry the one or two primitives of their leaves in leaf_a / leaf_b (-1 = none). */
+ * carry the one or two primitives of their leaves in leaf_a / leaf_b (-1 = none); nodes above it
+ * carry their split axis (0..2, drawn at build time) in leaf_a and -1 in leaf_b. */
 typedef struct rt_bvh_node {
   float lo[3];
   int32_t leaf_a;
@@ -158,6 +160,14 @@ enum rt_cam_mode {
   RT_CAM_PER_PIXEL = 1  /* lens/time draws from the pixel's own state                       */
 };
 
+/* rt_render_args.flags */
+#define RT_FLAG_EXACT_TRAVERSAL 1 /* visit exactly the reference's BVH node set (bvh.h:348-436)
+                                     instead of the margin-culled near-first traversal; both give
+                                     the same pixels, only node/prim test counts differ          */
+#define RT_FLAG_NO_LDS 4          /* keep the scene in global memory even when it fits in LDS   */
+#define RT_FLAG_AUDIT 2           /* run both traversals per BVH query, keep the exact result and
+                                     log every disagreement (read back with rt_audit_log)       */
+
 typedef struct rt_render_args {
   int32_t width, height;  /* full image size; N = width*height drives the RNG slots (H3)  */
   int32_t spp;            /* samples_per_pixel_per_fb (render.h:24)                      */
@@ -168,16 +178,17 @@ typedef struct rt_render_args {
   int32_t band_rows;      /* row tiling: rows grouped in bands of band_rows (>= 1)       */
   int32_t band_first;     /* this call renders bands b = band_first, +band_stride, ...   */
   int32_t band_stride;
-  int32_t stats;          /* 1: also count BVH node and primitive tests (slower)         */
-  int32_t pad;
+  int32_t stats;          /* 1: also count BVH node and primitive tests                  */
+  int32_t flags;          /* RT_FLAG_*                                                   */
   uint64_t seed;          /* 1984 in the reference (render.h:91)                         */
 } rt_render_args;
 
 typedef struct rt_counters {
   uint64_t segments;      /* top-level world->hit queries, primary + bounces (render.h:63) */
-  uint64_t node_tests;    /* stats only */
-  uint64_t prim_tests;    /* stats only */
+  uint64_t node_tests;    /* stats only: BVH box tests                                     */
+  uint64_t prim_tests;    /* stats only: primitive hit() tests                             */
   uint64_t samples;
+  uint64_t fallbacks;     /* stats only: culled BVH queries re-run on the reference visit set */
 } rt_counters;
 
 typedef struct rt_ctx rt_ctx;
@@ -201,6 +212,10 @@ int rt_render_init(rt_ctx* ctx, int32_t width, int32_t height, uint64_t seed);
 int rt_render(rt_ctx* ctx, const rt_render_args* args, float* fb_dev, rt_counters* counters);
 /* Duration in ms of the last render kernel, from HIP events recorded on the context stream. */
 float rt_last_render_ms(const rt_ctx* ctx);
+/* Audit log of the last RT_FLAG_AUDIT render: 16 floats per disagreeing BVH query (ray o[3] d[3]
+ * time, tmin, tmax, culled t, culled prim (int bits), exact t, exact prim, culled rank, 0, 0).
+ * Copies up to cap entries into out (may be NULL); returns the total number of disagreements. */
+int rt_audit_log(rt_ctx* ctx, float* out, int32_t cap);
 
 /* Quantise each fb (write_frame_buffer) and square-average them in fb order (average_images)
  * for the owned rows: out_dev = DEVICE pointer, [owned_rows][width][3] bytes, owned rows

@@ -27,6 +27,9 @@ LIB_PATH = os.path.join(_PKG, "librt_hip.so")
 
 RT_CAM_REF_SLOT0 = 0
 RT_CAM_PER_PIXEL = 1
+RT_FLAG_EXACT_TRAVERSAL = 1
+RT_FLAG_AUDIT = 2
+RT_FLAG_NO_LDS = 4
 
 PRIM_SPHERE, PRIM_MOVING_SPHERE, PRIM_RECT_XY, PRIM_RECT_XZ, PRIM_RECT_YZ, PRIM_TRIANGLE = range(6)
 OBJ_PRIM, OBJ_LIST, OBJ_BVH, OBJ_XFORM, OBJ_MEDIUM = range(5)
@@ -81,12 +84,12 @@ class rt_render_args(ctypes.Structure):
     _fields_ = [("width", c_int32), ("height", c_int32), ("spp", c_int32), ("fb_first", c_int32),
                 ("fb_count", c_int32), ("max_depth", c_int32), ("cam_mode", c_int32),
                 ("band_rows", c_int32), ("band_first", c_int32), ("band_stride", c_int32),
-                ("stats", c_int32), ("pad", c_int32), ("seed", c_uint64)]
+                ("stats", c_int32), ("flags", c_int32), ("seed", c_uint64)]
 
 
 class rt_counters(ctypes.Structure):
     _fields_ = [("segments", c_uint64), ("node_tests", c_uint64), ("prim_tests", c_uint64),
-                ("samples", c_uint64)]
+                ("samples", c_uint64), ("fallbacks", c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
@@ -102,6 +105,7 @@ ABI = {
     "rt_render_init": (c_int, [c_void_p, c_int32, c_int32, c_uint64]),
     "rt_render": (c_int, [c_void_p, POINTER(rt_render_args), c_void_p, POINTER(rt_counters)]),
     "rt_last_render_ms": (c_float, [c_void_p]),
+    "rt_audit_log": (c_int, [c_void_p, POINTER(c_float), c_int32]),
     "rt_resolve": (c_int, [c_void_p, POINTER(rt_render_args), c_void_p, c_void_p]),
     "rt_draw": (c_int, [c_void_p, POINTER(rt_render_args), POINTER(c_uint8), POINTER(rt_counters)]),
     "rt_scene_build": (c_int, [c_char_p, POINTER(c_void_p)]),
@@ -218,10 +222,12 @@ def scene(name: str) -> Scene:
 # ---------------------------------------------------------------- context (C ABI wrapper)
 def make_args(width: int, height: int, spp: int, fb_first: int = 0, fb_count: int = 1, max_depth: int = 50,
               cam_mode: int = RT_CAM_REF_SLOT0, band_rows: int = 0, band_first: int = 0, band_stride: int = 1,
-              stats: bool = False, seed: int = 1984) -> rt_render_args:
+              stats: bool = False, seed: int = 1984, exact: bool = False, audit: bool = False,
+              lds: bool = True) -> rt_render_args:
+    flags = (RT_FLAG_EXACT_TRAVERSAL if exact else 0) | (RT_FLAG_AUDIT if audit else 0) | (0 if lds else RT_FLAG_NO_LDS)
     return rt_render_args(width, height, spp, fb_first, fb_count, max_depth, cam_mode,
                           band_rows if band_rows > 0 else height, band_first, band_stride,
-                          1 if stats else 0, 0, seed)
+                          1 if stats else 0, flags, seed)
 
 
 def owned_rows(args: rt_render_args) -> np.ndarray:
@@ -265,6 +271,14 @@ class Context:
 
     def last_render_ms(self) -> float:
         return float(lib().rt_last_render_ms(self._c))
+
+    def audit_log(self, cap: int = 4096) -> tuple[int, np.ndarray]:
+        """(number of disagreements, [min(n, cap), 16] float32 entries) of the last audit render."""
+        buf = np.zeros((cap, 16), np.float32)
+        n = lib().rt_audit_log(self._c, buf.ctypes.data_as(POINTER(c_float)), cap)
+        if n < 0:
+            raise RtError("rt_audit_log failed")
+        return n, buf[: min(n, cap)].copy()
 
     def draw_args(self, args: rt_render_args) -> tuple[np.ndarray, dict]:
         img = np.zeros((args.height, args.width, 3), dtype=np.uint8)

@@ -33,6 +33,7 @@
 
 #include "../../include/rt_hip.h"
 #include "rt_detmath.h"
+#include "rt_host_geom.h"
 #include "rt_xorwow.h"
 
 #define RT_PRIM_TYPE_MASK 0xff
@@ -52,8 +53,12 @@ enum : int {
   F_NOISE = 1 << 8,
   F_IMAGE = 1 << 9,
   F_BVH = 1 << 10,
+  F_EXACT = 1 << 11,  // reference BVH visit set (no culling): node/prim counts equal the oracle's
+  F_CHECK = 1 << 12,  // culled search + exact re-run per query; disagreements logged (audit mode)
+  F_LDS = 1 << 13,    // BVH nodes + primitives staged in LDS (1024-thread workgroups, 1 per CU)
   F_ALL = (1 << 11) - 2,
-  F_SPHERES = F_MOVING | F_CHECKER | F_BVH,  // basic, first, big1 (C2), two_spheres
+  F_SPHERES = F_MOVING | F_CHECKER | F_BVH,           // basic, first, big1 (C2), two_spheres
+  F_CORNELL = F_RECT | F_LIST | F_XFORM | F_MEDIUM,   // cornell, cornell_smoke (C3)
 };
 
 namespace {
@@ -70,11 +75,32 @@ struct DScene {
   const rt_perlin* perlins;
   const rt_image* images;
   const uint8_t* texels;
+  float* dbg;            // audit log (F_CHECK): 16 floats per disagreeing BVH query
+  unsigned* dbg_n;
+  int32_t dbg_cap;
   int32_t n_world;
-  int32_t pad;
+  int32_t lds_nodes;     // F_LDS: node count staged (the primitives follow them)
+  int32_t pad2;
   rt_camera cam;
   float bg[3];
 };
+
+// LDS image of the scene for F_LDS variants: [nodes (2 float4 each) | prims (3 float4 each)].
+extern __shared__ float4 rt_lds[];
+
+// Node / primitive arrays: LDS for F_LDS variants, global memory otherwise.  Going through these
+// (instead of storing an LDS pointer into the scene struct) keeps the address space visible to
+// the compiler: ds_read for LDS, global_load for the kernel-argument pointers.
+template <int F>
+__device__ __forceinline__ const float4* nodes_of(const DScene& S) {
+  if constexpr ((F & F_LDS) != 0) return rt_lds;
+  else return S.nodes;
+}
+template <int F>
+__device__ __forceinline__ const float4* prims_of(const DScene& S) {
+  if constexpr ((F & F_LDS) != 0) return rt_lds + 2 * S.lds_nodes;
+  else return S.prims;
+}
 
 struct V {
   float x, y, z;
@@ -134,8 +160,9 @@ __device__ V in_unit_disk(Rng& s) {
 struct PrimRec {
   float4 a, b, c;
 };
+template <int F>
 __device__ __forceinline__ PrimRec load_prim(const DScene& S, int i) {
-  const float4* q = S.prims + 3 * i;
+  const float4* q = prims_of<F>(S) + 3 * i;
   return PrimRec{q[0], q[1], q[2]};
 }
 __device__ __forceinline__ int prim_type(const PrimRec& q) { return __float_as_int(q.c.z) & RT_PRIM_TYPE_MASK; }
@@ -200,10 +227,9 @@ __device__ __forceinline__ bool tri_t(const Ray& r, const rt_triangle& T, float 
 }
 
 template <int F>
-__device__ __forceinline__ bool prim_t(const DScene& S, int pi, const Ray& r, float tmin, float tmax, float& t,
-                                       unsigned& nprim) {
+__device__ __forceinline__ bool prim_t_q(const DScene& S, const PrimRec& q, const Ray& r, float tmin, float tmax,
+                                         float& t, unsigned& nprim) {
   if constexpr ((F & F_STATS) != 0) ++nprim;
-  const PrimRec q = load_prim(S, pi);
   const int type = prim_type(q);
   float bu, bv;
   if (type == RT_PRIM_SPHERE) return sphere_t(r, mk(q.a.x, q.a.y, q.a.z), q.a.w, tmin, tmax, t);
@@ -215,11 +241,16 @@ __device__ __forceinline__ bool prim_t(const DScene& S, int pi, const Ray& r, fl
     if (type >= RT_PRIM_RECT_XY && type <= RT_PRIM_RECT_YZ) return rect_t(r, q, type, tmin, tmax, t);
   return false;
 }
+template <int F>
+__device__ __forceinline__ bool prim_t(const DScene& S, int pi, const Ray& r, float tmin, float tmax, float& t,
+                                       unsigned& nprim) {
+  return prim_t_q<F>(S, load_prim<F>(S, pi), r, tmin, tmax, t, nprim);
+}
 
 // Full hit record of primitive pi at parameter t (the fields hit() sets on success).
 template <int F>
 __device__ void finalize(const DScene& S, int pi, const Ray& r, float t, Hit& h) {
-  const PrimRec q = load_prim(S, pi);
+  const PrimRec q = load_prim<F>(S, pi);
   const int tw = __float_as_int(q.c.z);
   const int type = tw & RT_PRIM_TYPE_MASK;
   h.t = t;
@@ -293,56 +324,210 @@ __device__ __forceinline__ bool box_hit(float4 lo, float4 hi, const Ray& r, V in
   return slab(lo.z, hi.z, r.o.z, inv.z, tmin, tmax);
 }
 
-// Closest primitive of a reference-layout BVH: every box is tested against the caller's
-// [tmin, tmax] (no shrinking), leaves keep strictly smaller t, visit order = depth-first,
-// left child first — identical candidate set and tie-breaking to the reference.
+// Conservative box test for the traversal tree: fma form, NaN-tolerant min/max, inclusive.
+// Returns the entry distance in tn.
+__device__ __forceinline__ bool fbox(float4 lo, float4 hi, V oi, V inv, float tmin, float tcut, float& tn) {
+  const float x0 = __builtin_fmaf(lo.x, inv.x, -oi.x), x1 = __builtin_fmaf(hi.x, inv.x, -oi.x);
+  const float y0 = __builtin_fmaf(lo.y, inv.y, -oi.y), y1 = __builtin_fmaf(hi.y, inv.y, -oi.y);
+  const float z0 = __builtin_fmaf(lo.z, inv.z, -oi.z), z1 = __builtin_fmaf(hi.z, inv.z, -oi.z);
+  const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x0, x1), __builtin_fminf(y0, y1)),
+                                      __builtin_fmaxf(__builtin_fminf(z0, z1), tmin));
+  const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x0, x1), __builtin_fmaxf(y0, y1)),
+                                     __builtin_fminf(__builtin_fmaxf(z0, z1), tcut));
+  tn = tnear;
+  return tnear <= tfar;
+}
+
+// Closest primitive of a reference-layout BVH with the reference's exact visit set: a node's box
+// is tested iff its parent's box passed (bvh.h:348-436), against the caller's [tmin, tmax],
+// depth-first, left first; leaves keep strictly smaller t (first hit wins ties).  Both children
+// of a node are tested from one 64-byte fetch (siblings are adjacent in heap order), halving the
+// chain of dependent loads; `pending` keeps, per level, whether a right child is still to visit.
 template <int F>
-__device__ bool bvh_closest(const DScene& S, int base, int rows, const Ray& r, float tmin, float tmax, float& best,
-                            int& best_prim, unsigned& nnode, unsigned& nprim) {
-  const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+__device__ bool bvh_exact(const DScene& S, int base, int rows, const Ray& r, V inv, float tmin, float tmax,
+                          float& best, int& best_prim, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   const int last0 = (1 << (rows - 1)) - 1;
   best = __builtin_inff();
   best_prim = -1;
-  int k = 0;
+  if constexpr ((F & F_STATS) != 0) ++nnode;
+  {
+    const float4 lo = nodes_of<F>(S)[2 * base], hi = nodes_of<F>(S)[2 * base + 1];
+    if (!box_hit(lo, hi, r, inv, tmin, tmax)) return false;
+  }
+  unsigned pending = 0;
+  int level = 0, k = 0;
   for (;;) {
-    if constexpr ((F & F_STATS) != 0) ++nnode;
-    const float4 lo = S.nodes[2 * (base + k)];
-    const float4 hi = S.nodes[2 * (base + k) + 1];
-    bool down = false;
-    if (box_hit(lo, hi, r, inv, tmin, tmax)) {
-      if (k >= last0) {
-        float t;
-        const int pa = __float_as_int(lo.w), pb = __float_as_int(hi.w);
-        if (prim_t<F>(S, pa, r, tmin, tmax, t, nprim) && t < best) {
-          best = t;
-          best_prim = pa;
-        }
-        if (pb >= 0 && prim_t<F>(S, pb, r, tmin, tmax, t, nprim) && t < best) {
-          best = t;
-          best_prim = pb;
-        }
-      } else {
-        down = true;
+    // invariant: the box of node k passed
+    if (k >= last0) {
+      const float4 lo = nodes_of<F>(S)[2 * (base + k)], hi = nodes_of<F>(S)[2 * (base + k) + 1];
+      float t;
+      const int pa = __float_as_int(lo.w), pb = __float_as_int(hi.w);
+      if (prim_t<F>(S, pa, r, tmin, tmax, t, nprim) && t < best) {
+        best = t;
+        best_prim = pa;
+      }
+      if (pb >= 0 && prim_t<F>(S, pb, r, tmin, tmax, t, nprim) && t < best) {
+        best = t;
+        best_prim = pb;
+      }
+    } else {
+      const float4* c = nodes_of<F>(S) + 2 * (base + 2 * k + 1);
+      const float4 l0 = c[0], l1 = c[1], r0 = c[2], r1 = c[3];
+      if constexpr ((F & F_STATS) != 0) nnode += 2;
+      const bool hl = box_hit(l0, l1, r, inv, tmin, tmax);
+      const bool hr = box_hit(r0, r1, r, inv, tmin, tmax);
+      if (hl || hr) {
+        pending = (pending & ~(1u << level)) | ((hl && hr) ? (1u << level) : 0u);
+        ++level;
+        k = 2 * k + (hl ? 1 : 2);
+        continue;
       }
     }
-    if (down) {
-      k = 2 * k + 1;
-    } else {
-      while (k > 0 && (k & 1) == 0) k = (k - 1) >> 1;
-      if (k == 0) break;
-      k += 1;
+    for (;;) {  // climb to the deepest level with a pending right child
+      if (level == 0) return best_prim >= 0;
+      --level;
+      k = (k - 1) >> 1;
+      if (pending & (1u << level)) {
+        pending &= ~(1u << level);
+        ++level;
+        k = 2 * k + 2;
+        break;
+      }
     }
   }
-  return best_prim >= 0;
+}
+
+// Closest primitive of a reference BVH object, same result as bvh_exact.
+//  1. Candidate search on the object's traversal tree (built at upload: same perfect-tree shape,
+//     largest-extent median splits, boxes padded by 2^-16 relative): both children per 64-byte
+//     fetch, nearer child first, boxes culled once their entry exceeds best*(1+2^-8).  Every
+//     primitive lies inside its padded ancestors, so a culled primitive's hit distance exceeds
+//     the box entry up to rounding (<= ~4e-4 relative for grazing spheres): strictly farther
+//     than best, it could not have won.  Ties go to the lower rank in the reference's depth-first
+//     left-first leaf order (first hit wins, bvh.h:375).
+//  2. The candidate wins in the reference iff the reference visits it: its last-row node and every
+//     ancestor pass the reference slab test against [tmin, tmax].  If that check fails (a
+//     floating-point edge of the reference's own boxes), the query is re-run on the exact visit set.
+template <int F>
+__device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, float tmin, float tmax, float& best,
+                            int& best_prim, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+  const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+  const int base = o.a, rows = o.b;
+  if constexpr ((F & F_EXACT) != 0) {
+    return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
+  } else {
+    const int last0 = (1 << (rows - 1)) - 1;
+    const int fb = o.c;
+    // Finite reciprocals for the traversal tree: with d = 0 the fma form would give inf - inf.
+    // Clamped to +-1e30 the slab of a parallel axis is (-huge, +huge) inside and empty outside.
+    const V finv = mk(__builtin_fminf(__builtin_fmaxf(inv.x, -1e30f), 1e30f),
+                      __builtin_fminf(__builtin_fmaxf(inv.y, -1e30f), 1e30f),
+                      __builtin_fminf(__builtin_fmaxf(inv.z, -1e30f), 1e30f));
+    const V oi = mk(r.o.x * finv.x, r.o.y * finv.y, r.o.z * finv.z);
+    best = __builtin_inff();
+    best_prim = -1;
+    int best_rank = 0x7fffffff;
+    unsigned pend = 0, far_right = 0;
+    int level = 0, k = 0;
+    bool walking = true;
+    while (walking) {
+      if (k >= last0) {
+        const float4 lo = nodes_of<F>(S)[2 * (fb + k)], hi = nodes_of<F>(S)[2 * (fb + k) + 1];
+        const int pa = __float_as_int(lo.w), pb = __float_as_int(hi.w);
+        float t;
+        PrimRec q = load_prim<F>(S, pa);
+        if (prim_t_q<F>(S, q, r, tmin, tmax, t, nprim)) {
+          const int rk = __float_as_int(q.c.y);
+          if (t < best || (t == best && rk < best_rank)) {
+            best = t;
+            best_prim = pa;
+            best_rank = rk;
+          }
+        }
+        if (pb >= 0) {
+          q = load_prim<F>(S, pb);
+          if (prim_t_q<F>(S, q, r, tmin, tmax, t, nprim)) {
+            const int rk = __float_as_int(q.c.y);
+            if (t < best || (t == best && rk < best_rank)) {
+              best = t;
+              best_prim = pb;
+              best_rank = rk;
+            }
+          }
+        }
+      } else {
+        const float4* c = nodes_of<F>(S) + 2 * (fb + 2 * k + 1);
+        const float4 l0 = c[0], l1 = c[1], r0 = c[2], r1 = c[3];
+        if constexpr ((F & F_STATS) != 0) nnode += 2;
+        const float cut = __builtin_fminf(best * 1.00390625f, tmax);
+        float tl, tr;
+        const bool hl = fbox(l0, l1, oi, finv, tmin, cut, tl);
+        const bool hr = fbox(r0, r1, oi, finv, tmin, cut, tr);
+        if (hl || hr) {
+          int next = hl ? 2 * k + 1 : 2 * k + 2;
+          if (hl && hr) {
+            const bool right_first = tr < tl;
+            pend |= 1u << level;
+            far_right = right_first ? (far_right & ~(1u << level)) : (far_right | (1u << level));
+            next = right_first ? 2 * k + 2 : 2 * k + 1;
+          }
+          ++level;
+          k = next;
+          continue;
+        }
+      }
+      for (;;) {  // climb to the deepest level with a pending far child
+        if (level == 0) {
+          walking = false;
+          break;
+        }
+        --level;
+        k = (k - 1) >> 1;
+        if (pend & (1u << level)) {
+          pend &= ~(1u << level);
+          k = 2 * k + 1 + (int)((far_right >> level) & 1u);
+          ++level;
+          break;
+        }
+      }
+    }
+    if constexpr ((F & F_CHECK) != 0) {
+      float te;
+      int pe;
+      bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, te, pe, nnode, nprim, nfall);
+      if (pe != best_prim || (pe >= 0 && __float_as_uint(te) != __float_as_uint(best))) {
+        const unsigned slot = atomicAdd(S.dbg_n, 1u);
+        if ((int)slot < S.dbg_cap) {
+          float* e = S.dbg + 16 * slot;
+          e[0] = r.o.x; e[1] = r.o.y; e[2] = r.o.z; e[3] = r.d.x; e[4] = r.d.y; e[5] = r.d.z; e[6] = r.tm;
+          e[7] = tmin; e[8] = tmax; e[9] = best; e[10] = __int_as_float(best_prim); e[11] = te;
+          e[12] = __int_as_float(pe); e[13] = __int_as_float(best_rank); e[14] = 0.0f; e[15] = 0.0f;
+        }
+      }
+      best = te;
+      best_prim = pe;
+      return pe >= 0;
+    }
+    if (best_prim < 0) return false;
+    for (int kr = last0 + (best_rank >> 1);; kr = (kr - 1) >> 1) {
+      if constexpr ((F & F_STATS) != 0) ++nnode;
+      const float4 lo = nodes_of<F>(S)[2 * (base + kr)], hi = nodes_of<F>(S)[2 * (base + kr) + 1];
+      if (!box_hit(lo, hi, r, inv, tmin, tmax)) {
+        if constexpr ((F & F_STATS) != 0) ++nfall;
+        return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
+      }
+      if (kr == 0) return true;
+    }
+  }
 }
 
 // Closest hit of a PRIM / LIST / BVH object: (t, prim).  LIST keeps the reference list rule:
 // shrinking t_max, later object wins ties (hittable_list.h:23-39).
 template <int F>
 __device__ bool leaf_closest(const DScene& S, const rt_object& o, const Ray& r, float tmin, float tmax, float& t,
-                             int& prim, unsigned& nnode, unsigned& nprim) {
+                             int& prim, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   if constexpr ((F & F_BVH) != 0)
-    if (o.kind == RT_OBJ_BVH) return bvh_closest<F>(S, o.a, o.b, r, tmin, tmax, t, prim, nnode, nprim);
+    if (o.kind == RT_OBJ_BVH) return bvh_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall);
   if (o.kind == RT_OBJ_PRIM || (F & F_LIST) == 0) {
     prim = o.a;
     return prim_t<F>(S, o.a, r, tmin, tmax, t, nprim);
@@ -378,20 +563,20 @@ __device__ __forceinline__ Ray xform_ray(const rt_object& o, const Ray& r, Ray& 
 // t of the closest hit of an object that may be an XFORM over a leaf object.
 template <int F>
 __device__ bool xform_closest_t(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t,
-                                unsigned& nnode, unsigned& nprim) {
+                                unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   const rt_object o = S.objects[oi];
   int prim;
-  if (o.kind != RT_OBJ_XFORM) return leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim);
+  if (o.kind != RT_OBJ_XFORM) return leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall);
   Ray moved;
   const Ray rr = xform_ray(o, r, moved);
   const rt_object c = S.objects[o.a];
-  return leaf_closest<F>(S, c, rr, tmin, tmax, t, prim, nnode, nprim);
+  return leaf_closest<F>(S, c, rr, tmin, tmax, t, prim, nnode, nprim, nfall);
 }
 
 // hittable::hit of one top-level object with a complete record.
 template <int F>
 __device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, float tmax, Hit& h, Rng& rng,
-                           unsigned& nnode, unsigned& nprim) {
+                           unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   const rt_object o = S.objects[oi];
   float t;
   int prim;
@@ -399,7 +584,7 @@ __device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, fl
       Ray moved;
       const Ray rr = xform_ray(o, r, moved);
       const rt_object c = S.objects[o.a];
-      if (!leaf_closest<F>(S, c, rr, tmin, tmax, t, prim, nnode, nprim)) return false;
+      if (!leaf_closest<F>(S, c, rr, tmin, tmax, t, prim, nnode, nprim, nfall)) return false;
       finalize<F>(S, prim, rr, t, h);
       if (o.b & 2) {
         const float s = o.f[3], cs = o.f[4];
@@ -417,8 +602,8 @@ __device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, fl
   if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {  // constant_medium.h:34-70 (one RNG draw per qualifying query, H8)
       const float inf = __builtin_inff();
       float t1, t2;
-      if (!xform_closest_t<F>(S, o.a, r, -inf, inf, t1, nnode, nprim)) return false;
-      if (!xform_closest_t<F>(S, o.a, r, t1 + 0.0001f, inf, t2, nnode, nprim)) return false;
+      if (!xform_closest_t<F>(S, o.a, r, -inf, inf, t1, nnode, nprim, nfall)) return false;
+      if (!xform_closest_t<F>(S, o.a, r, t1 + 0.0001f, inf, t2, nnode, nprim, nfall)) return false;
       if (t1 < tmin) t1 = tmin;
       if (t2 > tmax) t2 = tmax;
       if (t1 >= t2) return false;
@@ -436,19 +621,19 @@ __device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, fl
       h.v = 0.0f;
       return true;
   }
-  if (!leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim)) return false;
+  if (!leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall)) return false;
   finalize<F>(S, prim, r, t, h);
   return true;
 }
 
 // World = hittable_list of top-level objects (render.h:63 with t in [0.001, inf)).
 template <int F>
-__device__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsigned& nnode, unsigned& nprim) {
+__device__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   bool any = false;
   float closest = __builtin_inff();
   for (int w = 0; w < S.n_world; ++w) {
     Hit tmp;
-    if (object_hit<F>(S, S.world[w], r, 0.001f, closest, tmp, rng, nnode, nprim)) {
+    if (object_hit<F>(S, S.world[w], r, 0.001f, closest, tmp, rng, nnode, nprim, nfall)) {
       any = true;
       closest = tmp.t;
       h = tmp;
@@ -601,10 +786,12 @@ struct RenderParams {
   unsigned long long total_items;
   long long npix;  // W*H of the full image
   int W, H, rows, spp, fb_first, max_depth, cam_mode, pad;
+  int lds_prims, pad3;  // F_LDS: primitive count staged
   uint32_t cam_state[6];
 };
 
 constexpr int kBlock = 256;
+constexpr int kAuditCap = 4096;
 constexpr int kRefill = 16;  // refill a wave once this many lanes are idle
 
 __device__ __forceinline__ unsigned lane_rank(unsigned long long mask) {
@@ -617,8 +804,20 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 }
 
 template <int F>
-__global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
+constexpr int render_block() {
+  return (F & F_LDS) != 0 ? 1024 : 256;
+}
+
+template <int F>
+__global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderParams P) {
   const DScene& S = P.S;
+  if constexpr ((F & F_LDS) != 0) {
+    // Stage nodes and primitives (read-only, scene-sized) in LDS once per workgroup.
+    const int nn = 2 * P.S.lds_nodes, np = 3 * P.lds_prims;
+    for (int q = threadIdx.x; q < nn; q += render_block<F>()) rt_lds[q] = P.S.nodes[q];
+    for (int q = threadIdx.x; q < np; q += render_block<F>()) rt_lds[nn + q] = P.S.prims[q];
+    __syncthreads();
+  }
   const unsigned lane = __lane_id();
   long long item = -1;  // -1: idle
   bool done = false;
@@ -627,7 +826,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
   Ray ray{};
   V att = mk(1, 1, 1), col = mk(0, 0, 0);
   unsigned long long nseg = 0, nsamp = 0;
-  unsigned nnode = 0, nprim = 0;
+  unsigned nnode = 0, nprim = 0, nfall = 0;
   const bool per_pixel = P.cam_mode == RT_CAM_PER_PIXEL;
   const rt_camera& C = S.cam;
 
@@ -689,7 +888,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
     Hit h;
     bool ended = false;
     V contrib;
-    if (!world_hit<F>(S, ray, h, loc, nnode, nprim)) {
+    if (!world_hit<F>(S, ray, h, loc, nnode, nprim, nfall)) {
       contrib = att * ld3(S.bg);
       ended = true;
     } else {
@@ -723,10 +922,11 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
   }
 
   const unsigned long long ws = wave_sum(nseg), wm = wave_sum(nsamp);
-  unsigned long long wn = 0, wp = 0;
+  unsigned long long wn = 0, wp = 0, wf = 0;
   if constexpr ((F & F_STATS) != 0) {
     wn = wave_sum(nnode);
     wp = wave_sum(nprim);
+    wf = wave_sum(nfall);
   }
   if (lane == 0) {
     atomicAdd(&P.counters[0], ws);
@@ -734,6 +934,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const RenderParams P) {
     if constexpr ((F & F_STATS) != 0) {
       atomicAdd(&P.counters[1], wn);
       atomicAdd(&P.counters[2], wp);
+      atomicAdd(&P.counters[4], wf);
     }
   }
 }
@@ -804,9 +1005,11 @@ struct rt_ctx {
   unsigned long long* work = nullptr;  // [0] work counter, [1..4] counters
   int32_t* row_map = nullptr;
   int row_cap = 0;
-  int cus = 0, blocks_per_cu[8] = {0};
+  int cus = 0, blocks_per_cu[16] = {0};
   int features = 0;
+  int dev_nodes = 0, dev_prims = 0;  // device array sizes (for LDS staging)
   float last_ms = 0.0f;
+  float* dbg = nullptr;  // audit log: [0] = count, then 16 floats per entry
 };
 
 namespace {
@@ -815,22 +1018,47 @@ struct Variant {
   int mask;
   const void* fn;
 };
+#define RT_VARIANT(m) {m, (const void*)render_kernel<m>}
 const Variant kVariants[] = {
-    {F_SPHERES, (const void*)render_kernel<F_SPHERES>},
-    {F_ALL, (const void*)render_kernel<F_ALL>},
-    {F_SPHERES | F_STATS, (const void*)render_kernel<F_SPHERES | F_STATS>},
-    {F_ALL | F_STATS, (const void*)render_kernel<F_ALL | F_STATS>},
+    RT_VARIANT(F_SPHERES),
+    RT_VARIANT(F_ALL),
+    RT_VARIANT(F_SPHERES | F_STATS),
+    RT_VARIANT(F_ALL | F_STATS),
+    RT_VARIANT(F_SPHERES | F_EXACT),
+    RT_VARIANT(F_ALL | F_EXACT),
+    RT_VARIANT(F_SPHERES | F_EXACT | F_STATS),
+    RT_VARIANT(F_ALL | F_EXACT | F_STATS),
+    RT_VARIANT(F_SPHERES | F_CHECK),
+    RT_VARIANT(F_ALL | F_CHECK),
+    RT_VARIANT(F_SPHERES | F_LDS),
+    RT_VARIANT(F_ALL | F_LDS),
+    RT_VARIANT(F_CORNELL),
+    RT_VARIANT(F_CORNELL | F_EXACT | F_STATS),
 };
-constexpr int kNumVariants = 4;
+#undef RT_VARIANT
+constexpr int kNumVariants = 14;
+constexpr int kLdsBudget = 120 * 1024;  // bytes of nodes + primitives staged per workgroup
 
-// Smallest compiled variant that covers the scene's features.
-int pick_variant(int features, bool stats) {
-  for (int v = 0; v < kNumVariants; ++v) {
-    const int m = kVariants[v].mask;
-    if (((m & F_STATS) != 0) == stats && (features & ~m & ~F_STATS) == 0) return v;
+// Smallest compiled variant that covers the scene's features and the requested mode.
+int pick_variant(int features, bool stats, bool exact, bool check, bool lds) {
+  const int modes = F_STATS | F_EXACT | F_CHECK | F_LDS;
+  const int mode = check ? F_CHECK : ((stats ? F_STATS : 0) | (exact ? F_EXACT : 0));
+  auto best_of = [&](int want) {  // covering variant with the fewest feature bits
+    int best = -1;
+    for (int v = 0; v < kNumVariants; ++v) {
+      const int m = kVariants[v].mask;
+      if ((m & modes) != want || (features & ~m) != 0) continue;
+      if (best < 0 || __builtin_popcount(m) < __builtin_popcount(kVariants[best].mask)) best = v;
+    }
+    return best;
+  };
+  if (lds && mode == 0) {
+    const int v = best_of(F_LDS);
+    if (v >= 0) return v;
   }
-  return stats ? 3 : 1;
+  return best_of(mode);
 }
+int variant_block(int v) { return (kVariants[v].mask & F_LDS) != 0 ? 1024 : 256; }
 
 int scene_features(const rt_scene_soa* s) {
   int f = 0;
@@ -895,6 +1123,93 @@ bool tex_needs_uv(const rt_scene_soa* s, int ti) {
   return false;
 }
 
+// Traversal tree of a reference BVH (see bvh_closest): same perfect-tree shape and node counts as
+// the reference (so the device walks it with the same heap indexing), but every inner node splits
+// its primitives at the median along the largest extent of their box centres, and boxes are the
+// padded unions over the camera shutter.  Also writes each primitive's reference leaf rank (its
+// position in the reference's depth-first left-first order) into prims[].p[9].
+// Returns the first node index of the new tree in `nodes`, or -1 if the reference tree is malformed.
+int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<rt_prim>& prims,
+                         std::vector<rt_bvh_node>& nodes) {
+  const int inner = (1 << rows) - 1, last0 = (1 << (rows - 1)) - 1;
+  std::vector<int> members;
+  for (int k = last0; k < inner; ++k) {
+    const rt_bvh_node& nd = s->nodes[base + k];
+    const int ids[2] = {nd.leaf_a, nd.leaf_b};
+    for (int q = 0; q < 2; ++q) {
+      if (ids[q] < 0) continue;
+      if (ids[q] >= s->n_prims) return -1;
+      const int32_t rank = 2 * (k - last0) + q;
+      memcpy(&prims[ids[q]].p[9], &rank, 4);
+      members.push_back(ids[q]);
+    }
+  }
+  const int n = (int)members.size();
+  if (n < 2 || n > (1 << rows)) return -1;
+  std::vector<int> num(inner);
+  num[0] = n;
+  for (int k = 1; k < inner; ++k) {
+    const int par = (k - 1) >> 1;
+    num[k] = (k & 1) ? num[par] / 2 : num[par] / 2 + num[par] % 2;
+  }
+  for (int k = last0; k < inner; ++k)
+    if (num[k] < 1 || num[k] > 2) return -1;
+  const float t0 = s->camera.time0, t1 = s->camera.time1;
+  std::vector<rth::Box> box(s->n_prims);
+  std::vector<float> ctr(3 * (size_t)s->n_prims);
+  for (int id : members) {
+    box[id] = rth::prim_box(prims[id], s->triangles, t0 < t1 ? t0 : t1, t0 < t1 ? t1 : t0);
+    for (int a = 0; a < 3; ++a) ctr[3 * id + a] = 0.5f * box[id].lo[a] + 0.5f * box[id].hi[a];
+  }
+  const int fb = (int)nodes.size();
+  nodes.resize(fb + inner);
+  std::vector<std::vector<int>> part(inner);
+  part[0] = members;
+  for (int k = 0; k < inner; ++k) {
+    std::vector<int>& m = part[k];
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int id : m)
+      for (int a = 0; a < 3; ++a) {
+        lo[a] = std::min(lo[a], ctr[3 * id + a]);
+        hi[a] = std::max(hi[a], ctr[3 * id + a]);
+      }
+    int ax = 0;
+    for (int a = 1; a < 3; ++a)
+      if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
+    std::stable_sort(m.begin(), m.end(), [&](int x, int y) { return ctr[3 * x + ax] < ctr[3 * y + ax]; });
+    rt_bvh_node& nd = nodes[fb + k];
+    nd.leaf_a = ax;
+    nd.leaf_b = -1;
+    if (k >= last0) {
+      nd.leaf_a = m[0];
+      if (num[k] == 2) nd.leaf_b = m[1];
+    } else {
+      const int nl = num[2 * k + 1];
+      part[2 * k + 1].assign(m.begin(), m.begin() + nl);
+      part[2 * k + 2].assign(m.begin() + nl, m.end());
+    }
+  }
+  std::vector<rth::Box> bb(inner);
+  for (int k = inner - 1; k >= 0; --k) {
+    if (k >= last0) {
+      bb[k] = box[nodes[fb + k].leaf_a];
+      if (nodes[fb + k].leaf_b >= 0) bb[k] = rth::join(bb[k], box[nodes[fb + k].leaf_b]);
+    } else {
+      bb[k] = rth::join(bb[2 * k + 1], bb[2 * k + 2]);
+    }
+  }
+  for (int k = 0; k < inner; ++k) {  // pad by 2^-16 of (|coordinate| + extent)
+    rt_bvh_node& nd = nodes[fb + k];
+    for (int a = 0; a < 3; ++a) {
+      const float pad = (std::max(std::fabs(bb[k].lo[a]), std::fabs(bb[k].hi[a])) + (bb[k].hi[a] - bb[k].lo[a])) *
+                        (1.0f / 65536.0f);
+      nd.lo[a] = bb[k].lo[a] - pad;
+      nd.hi[a] = bb[k].hi[a] + pad;
+    }
+  }
+  return fb;
+}
+
 int validate_args(rt_ctx* c, const rt_render_args* a) {
   if (!a) return fail(c, RT_ERR_ARG, "null args");
   if (a->width <= 0 || a->height <= 0 || a->spp <= 0 || a->fb_count <= 0 || a->fb_first < 0 || a->max_depth <= 0)
@@ -934,7 +1249,8 @@ int rt_ctx_create(int hip_device, rt_ctx** out) {
     chk(hipGetDeviceProperties(&prop, hip_device), "hipGetDeviceProperties");
     c->cus = prop.multiProcessorCount;
     for (int v = 0; v < kNumVariants; ++v)
-      chk(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->blocks_per_cu[v], kVariants[v].fn, kBlock, 0),
+      chk(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->blocks_per_cu[v], kVariants[v].fn, variant_block(v),
+                                                       (kVariants[v].mask & F_LDS) ? kLdsBudget : 0),
           "occupancy");
   }
   if (rc != RT_OK) {
@@ -954,6 +1270,7 @@ int rt_ctx_destroy(rt_ctx* c) {
   if (c->seq) (void)hipFree(c->seq);
   if (c->work) (void)hipFree(c->work);
   if (c->row_map) (void)hipFree(c->row_map);
+  if (c->dbg) (void)hipFree(c->dbg);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -994,11 +1311,24 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
     if (s->prims[k].material < 0 || s->prims[k].material >= s->n_materials)
       return fail(c, RT_ERR_SCENE, "prim material out of range");
   free_scene(c);
-  // Device copy of the primitives with the u,v flag folded into the type word.
+  // Device copies: primitives with the u,v flag folded into the type word and their reference
+  // leaf rank in p[9]; nodes = reference trees followed by the traversal trees built here.
   std::vector<rt_prim> prims(s->prims, s->prims + s->n_prims);
   for (rt_prim& p : prims) {
     const rt_material& m = s->materials[p.material];
     if (p.type == RT_PRIM_SPHERE && m.type != RT_MAT_DIELECTRIC && tex_needs_uv(s, m.texture)) p.type |= RT_PRIM_FLAG_UV;
+    int32_t none = -1;
+    memcpy(&p.p[9], &none, 4);
+  }
+  std::vector<rt_bvh_node> nodes(s->nodes, s->nodes + s->n_nodes);
+  std::vector<rt_object> objects(s->objects, s->objects + s->n_objects);
+  for (rt_object& o : objects) {
+    o.c = -1;
+    if (o.kind == RT_OBJ_BVH) {
+      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes);
+      if (fast < 0) return fail(c, RT_ERR_SCENE, "malformed reference bvh");
+      o.c = fast;
+    }
   }
   DScene& d = c->scene;
   d = DScene{};
@@ -1007,10 +1337,10 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   const rt_material* dm;
   int rc;
   if ((rc = upload(c, s->world, (size_t)s->n_world, &d.world))) return rc;
-  if ((rc = upload(c, s->objects, (size_t)s->n_objects, &d.objects))) return rc;
+  if ((rc = upload(c, objects.data(), objects.size(), &d.objects))) return rc;
   if ((rc = upload(c, prims.data(), prims.size(), &dp))) return rc;
   if ((rc = upload(c, s->triangles, (size_t)s->n_triangles, &d.tris))) return rc;
-  if ((rc = upload(c, s->nodes, (size_t)s->n_nodes, &dn))) return rc;
+  if ((rc = upload(c, nodes.data(), nodes.size(), &dn))) return rc;
   if ((rc = upload(c, s->materials, (size_t)s->n_materials, &dm))) return rc;
   if ((rc = upload(c, s->textures, (size_t)s->n_textures, &d.texs))) return rc;
   if ((rc = upload(c, s->perlins, (size_t)s->n_perlins, &d.perlins))) return rc;
@@ -1025,6 +1355,8 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   d.bg[1] = s->background[1];
   d.bg[2] = s->background[2];
   c->features = scene_features(s);
+  c->dev_nodes = (int)nodes.size();
+  c->dev_prims = (int)prims.size();
   c->have_scene = true;
   return RT_OK;
 }
@@ -1094,13 +1426,30 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   for (int k = 0; k < 5; ++k) P.cam_state[1 + k] = cs.v[k];
 
   const bool stats = a->stats != 0;
-  const int var = pick_variant(c->features, stats);
+  const bool check = (a->flags & RT_FLAG_AUDIT) != 0;
+  const size_t lds_bytes = (size_t)(2 * c->dev_nodes + 3 * c->dev_prims) * sizeof(float4);
+  const bool use_lds = lds_bytes <= (size_t)kLdsBudget && (a->flags & RT_FLAG_NO_LDS) == 0;
+  const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds);
+  if (check) {
+    if (!c->dbg) {
+      HIPCHK(c, hipMalloc((void**)&c->dbg, 16 * sizeof(float) * kAuditCap + 64));
+    }
+    HIPCHK(c, hipMemsetAsync(c->dbg, 0, 16 * sizeof(float) * kAuditCap + 64, c->stream));
+    P.S.dbg = c->dbg + 16;
+    P.S.dbg_n = (unsigned*)c->dbg;
+    P.S.dbg_cap = kAuditCap;
+  }
+  if (var < 0) return fail(c, RT_ERR_SCENE, "no kernel variant covers the scene features");
+  const int bs = variant_block(var);
+  const bool lds_var = (kVariants[var].mask & F_LDS) != 0;
+  P.S.lds_nodes = lds_var ? c->dev_nodes : 0;
+  P.lds_prims = lds_var ? c->dev_prims : 0;
   const long long resident = (long long)c->cus * std::max(1, c->blocks_per_cu[var]);
-  const long long need = (long long)((P.total_items + kBlock - 1) / kBlock);
+  const long long need = (long long)((P.total_items + bs - 1) / bs);
   const unsigned blocks = (unsigned)std::max(1LL, std::min(resident, need));
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   void* kargs[] = {&P};
-  HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(kBlock), kargs, 0, c->stream));
+  HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), kargs, lds_var ? lds_bytes : 0, c->stream));
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   unsigned long long host_cnt[8];
@@ -1112,6 +1461,7 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
     counters->node_tests = host_cnt[2];
     counters->prim_tests = host_cnt[3];
     counters->samples = host_cnt[4];
+    counters->fallbacks = host_cnt[5];
   }
   if (host_cnt[4] != (unsigned long long)a->spp * P.total_items)
     return fail(c, RT_ERR_HIP, "render kernel did not complete every sample");
@@ -1119,6 +1469,18 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
 }
 
 float rt_last_render_ms(const rt_ctx* c) { return c ? c->last_ms : 0.0f; }
+
+int rt_audit_log(rt_ctx* c, float* out, int32_t cap) {
+  if (!c) return -1;
+  if (!c->dbg) return 0;
+  if (hipSetDevice(c->device) != hipSuccess) return -1;
+  unsigned n = 0;
+  if (hipMemcpy(&n, c->dbg, 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  const int m = (int)std::min<unsigned>(n, (unsigned)std::min(cap, kAuditCap));
+  if (out && m > 0 && hipMemcpy(out, c->dbg + 16, (size_t)m * 16 * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return (int)n;
+}
 
 int rt_resolve(rt_ctx* c, const rt_render_args* a, const float* fb_dev, uint8_t* out_dev) {
   if (!c) return RT_ERR_ARG;

@@ -16,6 +16,7 @@
 
 #include "../../include/rt_hip.h"
 #include "rt_detmath.h"
+#include "rt_host_geom.h"
 #include "rt_xorwow.h"
 
 namespace {
@@ -170,31 +171,8 @@ struct rt_scene_host {
 
   // bounding_box(t0, t1) of a primitive (sphere.h:75-78, moving_sphere.h:61-66, aarect.h).
   Box3 pbox(int pi, float t0, float t1) const {
-    const rt_prim& q = prims[pi];
-    const float* p = q.p;
-    switch (q.type) {
-      case RT_PRIM_SPHERE: {
-        const F3 c = mk(p[0], p[1], p[2]), r = mk(p[3], p[3], p[3]);
-        return Box3{sub(c, r), add(c, r)};
-      }
-      case RT_PRIM_MOVING_SPHERE: {
-        const F3 c0 = mk(p[0], p[1], p[2]), d = mk(p[4], p[5], p[6]), r = mk(p[3], p[3], p[3]);
-        const F3 ca = add(c0, scale((t0 - p[7]) / p[8], d));
-        const F3 cb = add(c0, scale((t1 - p[7]) / p[8], d));
-        return join(Box3{sub(ca, r), add(ca, r)}, Box3{sub(cb, r), add(cb, r)});
-      }
-      case RT_PRIM_RECT_XY: return Box3{mk(p[0], p[2], p[4] - 0.0001f), mk(p[1], p[3], p[4] + 0.0001f)};
-      case RT_PRIM_RECT_XZ: return Box3{mk(p[0], p[4] - 0.0001f, p[3]), mk(p[1], p[4] + 0.0001f, p[3])};
-      case RT_PRIM_RECT_YZ: return Box3{mk(p[4] - 0.0001f, p[0], p[2]), mk(p[4] + 0.0001f, p[1], p[3])};
-      default: {
-        const rt_triangle& t = tris[(int)p[0]];
-        const F3 a = mk(t.v0[0], t.v0[1], t.v0[2]);
-        const F3 b = add(a, mk(t.e0[0], t.e0[1], t.e0[2]));
-        const F3 c = add(a, mk(t.e1[0], t.e1[1], t.e1[2]));
-        return Box3{mk(std::min({a.x, b.x, c.x}), std::min({a.y, b.y, c.y}), std::min({a.z, b.z, c.z})),
-                    mk(std::max({a.x, b.x, c.x}), std::max({a.y, b.y, c.y}), std::max({a.z, b.z, c.z}))};
-      }
-    }
+    const rth::Box b = rth::prim_box(prims[pi], tris.data(), t0, t1);
+    return Box3{mk(b.lo[0], b.lo[1], b.lo[2]), mk(b.hi[0], b.hi[1], b.hi[2])};
   }
 
   // Reference-layout BVH over prims [first, first+n) (bvh.h:163-346): perfect tree of
@@ -243,7 +221,7 @@ struct rt_scene_host {
       const std::vector<int>& rk = rank[axis[k]];
       std::sort(m.begin(), m.end(), [&](int x, int y) { return rk[x] < rk[y]; });
       rt_bvh_node& nd = nodes[base + k];
-      nd.leaf_a = -1;
+      nd.leaf_a = axis[k];  // inner nodes keep their split axis (near-first ordering)
       nd.leaf_b = -1;
       if (k >= last0) {
         nd.leaf_a = first + m[0];

@@ -25,17 +25,17 @@ SMALL = [
 ]
 
 
-def _gpu_render(rt, ctx, scene, W, H, spp, fb_first, fb_count, cam, depth=50, band=None):
+def _gpu_render(rt, ctx, scene, W, H, spp, fb_first, fb_count, cam, depth=50, band=None, exact=False):
     import torch
 
     sc = rt.Scene.builtin(scene)
     ctx.upload(sc)
     ctx.render_init(W, H, 1984)
     if band is None:
-        args = rt.make_args(W, H, spp, fb_first, fb_count, depth, cam)
+        args = rt.make_args(W, H, spp, fb_first, fb_count, depth, cam, exact=exact)
     else:
         args = rt.make_args(W, H, spp, fb_first, fb_count, depth, cam, band_rows=band[0], band_first=band[1],
-                            band_stride=band[2])
+                            band_stride=band[2], exact=exact)
     rows = rt.owned_rows(args)
     fb = torch.zeros(fb_count * len(rows) * W * 3, dtype=torch.float32, device="cuda")
     cnt = ctx.render(args, fb.data_ptr())
@@ -47,9 +47,10 @@ def _bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
+@pytest.mark.parametrize("exact", [False, True], ids=["culled", "exact"])
 @pytest.mark.parametrize("scene,W,H,spp,fb_first,fb_count,cam", SMALL)
-def test_small_bit_exact(rtlib, gpu_ctx, oracle, scene, W, H, spp, fb_first, fb_count, cam):
-    gpu, rows, cnt, _, _ = _gpu_render(rtlib, gpu_ctx, scene, W, H, spp, fb_first, fb_count, cam)
+def test_small_bit_exact(rtlib, gpu_ctx, oracle, scene, W, H, spp, fb_first, fb_count, cam, exact):
+    gpu, rows, cnt, _, _ = _gpu_render(rtlib, gpu_ctx, scene, W, H, spp, fb_first, fb_count, cam, exact=exact)
     ref = oracle.RefScene(scene)
     segs = 0
     for f in range(fb_count):
@@ -111,20 +112,36 @@ def test_full_size_row_subset(rtlib, gpu_ctx, oracle, scene, W, H, spp, rows):
 
 
 def test_stats_counters_match_oracle(rtlib, gpu_ctx, oracle):
-    """Node/primitive test counts of the stats variant equal the oracle's (same visit set)."""
+    """Node/primitive test counts of the exact-traversal stats variant equal the oracle's (the
+    reference's visit set); the culled traversal visits strictly fewer."""
     W, H, spp = 48, 27, 2
     import torch
 
     sc = rtlib.Scene.builtin("big1")
     gpu_ctx.upload(sc)
     gpu_ctx.render_init(W, H, 1984)
-    args = rtlib.make_args(W, H, spp, 0, 1, 50, REF, stats=True)
+    args = rtlib.make_args(W, H, spp, 0, 1, 50, REF, stats=True, exact=True)
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
     cnt = gpu_ctx.render(args, fb.data_ptr())
     _, c, _ = oracle.RefScene("big1").render(W, H, spp, 0, 50, REF)
     assert cnt["segments"] == c["segments"]
     assert cnt["node_tests"] == c["node_tests"]
     assert cnt["prim_tests"] == c["prim_tests"]
+    fast = gpu_ctx.render(rtlib.make_args(W, H, spp, 0, 1, 50, REF, stats=True), fb.data_ptr())
+    assert fast["segments"] == c["segments"] and fast["node_tests"] < c["node_tests"]
+
+
+@pytest.mark.parametrize("scene,W,H,spp,nfb", [
+    ("big1", 1200, 800, 10, 10),          # the whole C2 bench workload (100 rays/pixel)
+    ("cornell_smoke", 800, 800, 10, 2),   # C3 geometry, 20 rays/pixel
+])
+def test_culled_equals_exact_full_workload(rtlib, gpu_ctx, scene, W, H, spp, nfb):
+    """Over an entire benchmark workload the culled traversal reproduces the reference-visit-set
+    traversal bit for bit (every float of every fb) and with the same segment count."""
+    fast, _, cf, _, _ = _gpu_render(rtlib, gpu_ctx, scene, W, H, spp, 0, nfb, REF)
+    ex, _, ce, _, _ = _gpu_render(rtlib, gpu_ctx, scene, W, H, spp, 0, nfb, REF, exact=True)
+    assert cf["segments"] == ce["segments"]
+    assert np.array_equal(_bits(fast), _bits(ex))
 
 
 @pytest.mark.parametrize("key,scene,W,H,spp,fbs,depth", [
