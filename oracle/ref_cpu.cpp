@@ -226,6 +226,10 @@ struct Counters {
   long long seg = 0, node = 0, prim = 0, samples = 0;
 };
 static thread_local Counters* tl_cnt = nullptr;
+// Optional capture of world-query rays (o, d, tm) for offline tree experiments.
+static std::atomic<long long> g_cap_n{0};
+static long long g_cap_max = 0;
+static float* g_cap = nullptr;
 static thread_local bool tl_h20 = false;
 
 static inline int rand_int(Draw& g, int lo, int hi) {  // common.h:49-52 (may return hi+1: H20)
@@ -960,6 +964,13 @@ static V3 trace(const ref_scene& s, Ray r, Draw& g, int depth) {
   for (int i = 0; i < depth; ++i) {
     Rec rec;
     if (tl_cnt) tl_cnt->seg++;
+    if (g_cap) {
+      const long long k = g_cap_n.fetch_add(1);
+      if (k < g_cap_max) {
+        float* e = g_cap + 8 * k;
+        e[0] = r.o.x; e[1] = r.o.y; e[2] = r.o.z; e[3] = r.d.x; e[4] = r.d.y; e[5] = r.d.z; e[6] = r.tm; e[7] = 0;
+      }
+    }
     if (!s.world->hit(r, 0.001f, INFINITY, rec, g)) return att * s.background;
     Ray sc;
     V3 a;
@@ -1020,6 +1031,12 @@ int ref_scene_create(const char* name, int rtl, ref_scene** out) {
   return 0;
 }
 void ref_scene_destroy(ref_scene* s) { delete s; }
+long long ref_capture_rays(float* buf, long long max_rays) {  // buf = NULL stops capturing
+  const long long n = g_cap_n.exchange(0);
+  g_cap = buf;
+  g_cap_max = buf ? max_rays : 0;
+  return n;
+}
 float ref_scene_aspect(const ref_scene* s) { return s->aspect; }
 void ref_scene_background(const ref_scene* s, float rgb[3]) {
   rgb[0] = s->background.x;

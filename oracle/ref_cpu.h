@@ -26,6 +26,9 @@ enum { REF_CAM_REF_SLOT0 = 0, REF_CAM_PER_PIXEL = 1 };
  * right-to-left instead of left-to-right (hazard H9; used only for the layout pin test). */
 int ref_scene_create(const char* name, int rtl, ref_scene** out);
 void ref_scene_destroy(ref_scene* s);
+/* Capture world-query rays (8 floats: o, d, time, 0) into buf during later ref_render calls
+ * (design experiments only); returns the number captured since the previous call. */
+long long ref_capture_rays(float* buf, long long max_rays);
 float ref_scene_aspect(const ref_scene* s);
 void ref_scene_background(const ref_scene* s, float rgb[3]);
 int ref_scene_h20(const ref_scene* s); /* 1 if random_int returned max+1 during the build */

@@ -80,7 +80,7 @@ struct DScene {
   int32_t dbg_cap;
   int32_t n_world;
   int32_t lds_nodes;     // F_LDS: node count staged (the primitives follow them)
-  int32_t pad2;
+  int32_t lds_prims;     // F_LDS: primitive count staged (the traversal stacks follow them)
   rt_camera cam;
   float bg[3];
 };
@@ -101,6 +101,19 @@ __device__ __forceinline__ const float4* prims_of(const DScene& S) {
   if constexpr ((F & F_LDS) != 0) return rt_lds + 2 * S.lds_nodes;
   else return S.prims;
 }
+template <int F>
+constexpr int render_block() {
+  return (F & F_LDS) != 0 ? 1024 : 256;
+}
+template <int F>
+__device__ __forceinline__ int* stack_of(const DScene& S) {
+  if constexpr ((F & F_LDS) != 0) return (int*)(rt_lds + 2 * S.lds_nodes + 3 * S.lds_prims) + threadIdx.x;
+  else return (int*)rt_lds + threadIdx.x;
+}
+
+// Per-lane traversal stack in LDS (after the staged scene for F_LDS variants), lane-interleaved
+// (entry d of thread t at [d * block + t]) so a wave's pushes/pops hit 64 distinct banks.
+constexpr int kStackDepth = 16;
 
 struct V {
   float x, y, z;
@@ -417,7 +430,7 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
     return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
   } else {
     const int last0 = (1 << (rows - 1)) - 1;
-    const int fb = o.c;
+    const int fb = o.c;  // traversal tree: 64-byte records at nodes[fb + 2i], root i = 0
     // Finite reciprocals for the traversal tree: with d = 0 the fma form would give inf - inf.
     // Clamped to +-1e30 the slab of a parallel axis is (-huge, +huge) inside and empty outside.
     const V finv = mk(__builtin_fminf(__builtin_fmaxf(inv.x, -1e30f), 1e30f),
@@ -427,69 +440,55 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
     best = __builtin_inff();
     best_prim = -1;
     int best_rank = 0x7fffffff;
-    unsigned pend = 0, far_right = 0;
-    int level = 0, k = 0;
-    bool walking = true;
-    while (walking) {
-      if (k >= last0) {
-        const float4 lo = nodes_of<F>(S)[2 * (fb + k)], hi = nodes_of<F>(S)[2 * (fb + k) + 1];
-        const int pa = __float_as_int(lo.w), pb = __float_as_int(hi.w);
-        float t;
-        PrimRec q = load_prim<F>(S, pa);
-        if (prim_t_q<F>(S, q, r, tmin, tmax, t, nprim)) {
-          const int rk = __float_as_int(q.c.y);
-          if (t < best || (t == best && rk < best_rank)) {
-            best = t;
-            best_prim = pa;
-            best_rank = rk;
-          }
-        }
-        if (pb >= 0) {
-          q = load_prim<F>(S, pb);
+    int* stk = stack_of<F>(S);
+    constexpr int BS = render_block<F>();
+    int sp = 0, cur = 0;
+    bool overflow = false;
+    for (;;) {
+      const float4* n = nodes_of<F>(S) + 2 * (fb + 2 * cur);
+      const float4 l0 = n[0], l1 = n[1], r0 = n[2], r1 = n[3];
+      if constexpr ((F & F_STATS) != 0) nnode += 2;
+      const float cut = __builtin_fminf(best * 1.00390625f, tmax);
+      float tl, tr;
+      bool hl = fbox(l0, l1, oi, finv, tmin, cut, tl);
+      bool hr = fbox(r0, r1, oi, finv, tmin, cut, tr);
+      const int c0 = __float_as_int(l0.w), c1 = __float_as_int(l1.w);
+      // primitive children are tested right away (leaves hold one primitive)
+      #pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const int ch = side == 0 ? c0 : c1;
+        if ((side == 0 ? hl : hr) && ch < 0) {
+          const int pi = -ch - 1;
+          const PrimRec q = load_prim<F>(S, pi);
+          float t;
           if (prim_t_q<F>(S, q, r, tmin, tmax, t, nprim)) {
             const int rk = __float_as_int(q.c.y);
             if (t < best || (t == best && rk < best_rank)) {
               best = t;
-              best_prim = pb;
+              best_prim = pi;
               best_rank = rk;
             }
           }
-        }
-      } else {
-        const float4* c = nodes_of<F>(S) + 2 * (fb + 2 * k + 1);
-        const float4 l0 = c[0], l1 = c[1], r0 = c[2], r1 = c[3];
-        if constexpr ((F & F_STATS) != 0) nnode += 2;
-        const float cut = __builtin_fminf(best * 1.00390625f, tmax);
-        float tl, tr;
-        const bool hl = fbox(l0, l1, oi, finv, tmin, cut, tl);
-        const bool hr = fbox(r0, r1, oi, finv, tmin, cut, tr);
-        if (hl || hr) {
-          int next = hl ? 2 * k + 1 : 2 * k + 2;
-          if (hl && hr) {
-            const bool right_first = tr < tl;
-            pend |= 1u << level;
-            far_right = right_first ? (far_right & ~(1u << level)) : (far_right | (1u << level));
-            next = right_first ? 2 * k + 2 : 2 * k + 1;
-          }
-          ++level;
-          k = next;
-          continue;
+          if (side == 0) hl = false; else hr = false;
         }
       }
-      for (;;) {  // climb to the deepest level with a pending far child
-        if (level == 0) {
-          walking = false;
-          break;
-        }
-        --level;
-        k = (k - 1) >> 1;
-        if (pend & (1u << level)) {
-          pend &= ~(1u << level);
-          k = 2 * k + 1 + (int)((far_right >> level) & 1u);
-          ++level;
-          break;
-        }
+      if (hl && hr) {
+        const bool right_first = tr < tl;
+        if (sp < kStackDepth) stk[BS * sp++] = right_first ? c0 : c1;
+        else overflow = true;
+        cur = right_first ? c1 : c0;
+        continue;
       }
+      if (hl || hr) {
+        cur = hl ? c0 : c1;
+        continue;
+      }
+      if (sp == 0) break;
+      cur = stk[BS * --sp];
+    }
+    if (overflow) {  // a subtree was dropped: answer on the exact visit set instead
+      if constexpr ((F & F_STATS) != 0) ++nfall;
+      return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
     }
     if constexpr ((F & F_CHECK) != 0) {
       float te;
@@ -786,7 +785,7 @@ struct RenderParams {
   unsigned long long total_items;
   long long npix;  // W*H of the full image
   int W, H, rows, spp, fb_first, max_depth, cam_mode, pad;
-  int lds_prims, pad3;  // F_LDS: primitive count staged
+  int pad3, pad4;
   uint32_t cam_state[6];
 };
 
@@ -804,16 +803,11 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 }
 
 template <int F>
-constexpr int render_block() {
-  return (F & F_LDS) != 0 ? 1024 : 256;
-}
-
-template <int F>
 __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderParams P) {
   const DScene& S = P.S;
   if constexpr ((F & F_LDS) != 0) {
     // Stage nodes and primitives (read-only, scene-sized) in LDS once per workgroup.
-    const int nn = 2 * P.S.lds_nodes, np = 3 * P.lds_prims;
+    const int nn = 2 * P.S.lds_nodes, np = 3 * P.S.lds_prims;
     for (int q = threadIdx.x; q < nn; q += render_block<F>()) rt_lds[q] = P.S.nodes[q];
     for (int q = threadIdx.x; q < np; q += render_block<F>()) rt_lds[nn + q] = P.S.prims[q];
     __syncthreads();
@@ -1037,7 +1031,7 @@ const Variant kVariants[] = {
 };
 #undef RT_VARIANT
 constexpr int kNumVariants = 14;
-constexpr int kLdsBudget = 120 * 1024;  // bytes of nodes + primitives staged per workgroup
+constexpr int kLdsBudget = 156 * 1024;  // bytes of staged nodes + primitives + stacks per workgroup
 
 // Smallest compiled variant that covers the scene's features and the requested mode.
 int pick_variant(int features, bool stats, bool exact, bool check, bool lds) {
@@ -1123,12 +1117,90 @@ bool tex_needs_uv(const rt_scene_soa* s, int ti) {
   return false;
 }
 
-// Traversal tree of a reference BVH (see bvh_closest): same perfect-tree shape and node counts as
-// the reference (so the device walks it with the same heap indexing), but every inner node splits
-// its primitives at the median along the largest extent of their box centres, and boxes are the
-// padded unions over the camera shutter.  Also writes each primitive's reference leaf rank (its
+// Traversal tree of a reference BVH (see bvh_closest): a binary SAH tree over the same
+// primitives, one primitive per leaf, child boxes stored in the parent (padded by 2^-16 relative
+// so a primitive hit is never outside its padded ancestors).  Record i = 2 rt_bvh_node slots at
+// nodes[fb + 2i]: {lo0, child0}, {hi0, child1}, {lo1, -}, {hi1, -}; child >= 0 is a record,
+// child < 0 the primitive -child-1.  Also writes each primitive's reference leaf rank (its
 // position in the reference's depth-first left-first order) into prims[].p[9].
 // Returns the first node index of the new tree in `nodes`, or -1 if the reference tree is malformed.
+struct SahBuilder {
+  const std::vector<rth::Box>& box;
+  std::vector<rt_bvh_node>& nodes;
+  int fb;
+  static float area(const rth::Box& b) {
+    const float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+    return dx < 0.0f ? 0.0f : 2.0f * (dx * dy + dy * dz + dz * dx);
+  }
+  static rth::Box pad(rth::Box b) {
+    for (int a = 0; a < 3; ++a) {
+      const float p = (std::max(std::fabs(b.lo[a]), std::fabs(b.hi[a])) + (b.hi[a] - b.lo[a])) * (1.0f / 65536.0f);
+      b.lo[a] -= p;
+      b.hi[a] += p;
+    }
+    return b;
+  }
+  rth::Box bounds(const int* ids, int n) const {
+    rth::Box b = box[ids[0]];
+    for (int i = 1; i < n; ++i) b = rth::join(b, box[ids[i]]);
+    return b;
+  }
+  // Builds the subtree over ids[0..n) (n >= 2) as record `me`; returns nothing.
+  void build(int* ids, int n, int me) {
+    float best = INFINITY;
+    int bax = 0, bsplit = n / 2;
+    std::vector<float> right(n + 1);
+    for (int ax = 0; ax < 3; ++ax) {
+      auto key = [&](int id) { return box[id].lo[ax] + box[id].hi[ax]; };
+      std::stable_sort(ids, ids + n, [&](int x, int y) { return key(x) < key(y); });
+      rth::Box acc = box[ids[n - 1]];
+      for (int i = n - 1; i >= 1; --i) {
+        if (i < n - 1) acc = rth::join(acc, box[ids[i]]);
+        right[i] = area(acc) * (float)(n - i);
+      }
+      rth::Box lacc = box[ids[0]];
+      for (int i = 1; i < n; ++i) {
+        if (i > 1) lacc = rth::join(lacc, box[ids[i - 1]]);
+        const float cost = area(lacc) * (float)i + right[i];
+        if (cost < best) {
+          best = cost;
+          bax = ax;
+          bsplit = i;
+        }
+      }
+    }
+    auto key = [&](int id) { return box[id].lo[bax] + box[id].hi[bax]; };
+    std::stable_sort(ids, ids + n, [&](int x, int y) { return key(x) < key(y); });
+    int child[2];
+    rth::Box cb[2];
+    const int part[2][2] = {{0, bsplit}, {bsplit, n}};
+    for (int c = 0; c < 2; ++c) {
+      const int* cid = ids + part[c][0];
+      const int cn = part[c][1] - part[c][0];
+      cb[c] = pad(bounds(cid, cn));
+      if (cn == 1) {
+        child[c] = -cid[0] - 1;
+      } else {
+        child[c] = (int)(nodes.size() - fb) / 2;
+        nodes.resize(nodes.size() + 2);
+      }
+    }
+    rt_bvh_node* r = &nodes[fb + 2 * me];
+    for (int a = 0; a < 3; ++a) {
+      r[0].lo[a] = cb[0].lo[a];
+      r[0].hi[a] = cb[0].hi[a];
+      r[1].lo[a] = cb[1].lo[a];
+      r[1].hi[a] = cb[1].hi[a];
+    }
+    r[0].leaf_a = child[0];
+    r[0].leaf_b = child[1];
+    r[1].leaf_a = 0;
+    r[1].leaf_b = 0;
+    for (int c = 0; c < 2; ++c)
+      if (child[c] >= 0) build(ids + part[c][0], part[c][1] - part[c][0], child[c]);
+  }
+};
+
 int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<rt_prim>& prims,
                          std::vector<rt_bvh_node>& nodes) {
   const int inner = (1 << rows) - 1, last0 = (1 << (rows - 1)) - 1;
@@ -1146,67 +1218,13 @@ int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<
   }
   const int n = (int)members.size();
   if (n < 2 || n > (1 << rows)) return -1;
-  std::vector<int> num(inner);
-  num[0] = n;
-  for (int k = 1; k < inner; ++k) {
-    const int par = (k - 1) >> 1;
-    num[k] = (k & 1) ? num[par] / 2 : num[par] / 2 + num[par] % 2;
-  }
-  for (int k = last0; k < inner; ++k)
-    if (num[k] < 1 || num[k] > 2) return -1;
   const float t0 = s->camera.time0, t1 = s->camera.time1;
   std::vector<rth::Box> box(s->n_prims);
-  std::vector<float> ctr(3 * (size_t)s->n_prims);
-  for (int id : members) {
-    box[id] = rth::prim_box(prims[id], s->triangles, t0 < t1 ? t0 : t1, t0 < t1 ? t1 : t0);
-    for (int a = 0; a < 3; ++a) ctr[3 * id + a] = 0.5f * box[id].lo[a] + 0.5f * box[id].hi[a];
-  }
+  for (int id : members) box[id] = rth::prim_box(prims[id], s->triangles, t0 < t1 ? t0 : t1, t0 < t1 ? t1 : t0);
   const int fb = (int)nodes.size();
-  nodes.resize(fb + inner);
-  std::vector<std::vector<int>> part(inner);
-  part[0] = members;
-  for (int k = 0; k < inner; ++k) {
-    std::vector<int>& m = part[k];
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int id : m)
-      for (int a = 0; a < 3; ++a) {
-        lo[a] = std::min(lo[a], ctr[3 * id + a]);
-        hi[a] = std::max(hi[a], ctr[3 * id + a]);
-      }
-    int ax = 0;
-    for (int a = 1; a < 3; ++a)
-      if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
-    std::stable_sort(m.begin(), m.end(), [&](int x, int y) { return ctr[3 * x + ax] < ctr[3 * y + ax]; });
-    rt_bvh_node& nd = nodes[fb + k];
-    nd.leaf_a = ax;
-    nd.leaf_b = -1;
-    if (k >= last0) {
-      nd.leaf_a = m[0];
-      if (num[k] == 2) nd.leaf_b = m[1];
-    } else {
-      const int nl = num[2 * k + 1];
-      part[2 * k + 1].assign(m.begin(), m.begin() + nl);
-      part[2 * k + 2].assign(m.begin() + nl, m.end());
-    }
-  }
-  std::vector<rth::Box> bb(inner);
-  for (int k = inner - 1; k >= 0; --k) {
-    if (k >= last0) {
-      bb[k] = box[nodes[fb + k].leaf_a];
-      if (nodes[fb + k].leaf_b >= 0) bb[k] = rth::join(bb[k], box[nodes[fb + k].leaf_b]);
-    } else {
-      bb[k] = rth::join(bb[2 * k + 1], bb[2 * k + 2]);
-    }
-  }
-  for (int k = 0; k < inner; ++k) {  // pad by 2^-16 of (|coordinate| + extent)
-    rt_bvh_node& nd = nodes[fb + k];
-    for (int a = 0; a < 3; ++a) {
-      const float pad = (std::max(std::fabs(bb[k].lo[a]), std::fabs(bb[k].hi[a])) + (bb[k].hi[a] - bb[k].lo[a])) *
-                        (1.0f / 65536.0f);
-      nd.lo[a] = bb[k].lo[a] - pad;
-      nd.hi[a] = bb[k].hi[a] + pad;
-    }
-  }
+  nodes.resize(fb + 2);  // record 0 = root
+  SahBuilder sb{box, nodes, fb};
+  sb.build(members.data(), n, 0);
   return fb;
 }
 
@@ -1250,7 +1268,8 @@ int rt_ctx_create(int hip_device, rt_ctx** out) {
     c->cus = prop.multiProcessorCount;
     for (int v = 0; v < kNumVariants; ++v)
       chk(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->blocks_per_cu[v], kVariants[v].fn, variant_block(v),
-                                                       (kVariants[v].mask & F_LDS) ? kLdsBudget : 0),
+                                                       (kVariants[v].mask & F_LDS) ? kLdsBudget
+                                                                                   : variant_block(v) * kStackDepth * 4),
           "occupancy");
   }
   if (rc != RT_OK) {
@@ -1428,7 +1447,7 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   const bool stats = a->stats != 0;
   const bool check = (a->flags & RT_FLAG_AUDIT) != 0;
   const size_t lds_bytes = (size_t)(2 * c->dev_nodes + 3 * c->dev_prims) * sizeof(float4);
-  const bool use_lds = lds_bytes <= (size_t)kLdsBudget && (a->flags & RT_FLAG_NO_LDS) == 0;
+  const bool use_lds = lds_bytes + 1024 * kStackDepth * 4 <= (size_t)kLdsBudget && (a->flags & RT_FLAG_NO_LDS) == 0;
   const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds);
   if (check) {
     if (!c->dbg) {
@@ -1443,13 +1462,14 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   const int bs = variant_block(var);
   const bool lds_var = (kVariants[var].mask & F_LDS) != 0;
   P.S.lds_nodes = lds_var ? c->dev_nodes : 0;
-  P.lds_prims = lds_var ? c->dev_prims : 0;
+  P.S.lds_prims = lds_var ? c->dev_prims : 0;
+  const size_t shmem = (lds_var ? lds_bytes : 0) + (size_t)bs * kStackDepth * 4;
   const long long resident = (long long)c->cus * std::max(1, c->blocks_per_cu[var]);
   const long long need = (long long)((P.total_items + bs - 1) / bs);
   const unsigned blocks = (unsigned)std::max(1LL, std::min(resident, need));
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   void* kargs[] = {&P};
-  HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), kargs, lds_var ? lds_bytes : 0, c->stream));
+  HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), kargs, shmem, c->stream));
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   unsigned long long host_cnt[8];
