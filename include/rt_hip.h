@@ -205,6 +205,9 @@ int rt_scene_upload(rt_ctx* ctx, const rt_scene_soa* scene);
 
 /* Per-slot XORWOW states curand_init(seed, slot, 0) for slot < width*height (render.h:84-92). */
 int rt_render_init(rt_ctx* ctx, int32_t width, int32_t height, uint64_t seed);
+/* Copies states [first, first+count) to host as 6 words each: d, v0..v4 (the curandStateXORWOW
+ * words the reference's render_init leaves in its state array). */
+int rt_read_states(rt_ctx* ctx, int64_t first, int64_t count, uint32_t* out);
 
 /* Renders fb ids [fb_first, fb_first+fb_count) for the owned rows into fb_dev (a DEVICE
  * pointer): layout [fb_count][owned_rows][width][3] floats, owned rows ascending.

@@ -103,6 +103,7 @@ ABI = {
     "rt_owned_rows": (c_int32, [POINTER(rt_render_args), POINTER(c_int32)]),
     "rt_scene_upload": (c_int, [c_void_p, POINTER(rt_scene_soa)]),
     "rt_render_init": (c_int, [c_void_p, c_int32, c_int32, c_uint64]),
+    "rt_read_states": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
     "rt_render": (c_int, [c_void_p, POINTER(rt_render_args), c_void_p, POINTER(rt_counters)]),
     "rt_last_render_ms": (c_float, [c_void_p]),
     "rt_audit_log": (c_int, [c_void_p, POINTER(c_float), c_int32]),
@@ -258,6 +259,11 @@ class Context:
 
     def render_init(self, width: int, height: int, seed: int = 1984) -> None:
         self._check(lib().rt_render_init(self._c, width, height, seed), "rt_render_init")
+
+    def read_states(self, first: int, count: int) -> np.ndarray:
+        out = np.zeros((count, 6), np.uint32)
+        self._check(lib().rt_read_states(self._c, first, count, out.ctypes.data), "rt_read_states")
+        return out
 
     def render(self, args: rt_render_args, fb_dev_ptr: int) -> dict:
         cnt = rt_counters()

@@ -933,15 +933,17 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
   }
 }
 
-// curand_init(seed, slot, 0) for every slot < n (render.h:84-92): seed scramble, then the
-// subsequence jump A^(slot * 2^67) applied digit by digit in base 4 (as skipahead_sequence).
-// The jump matrix of each digit position is wave-uniform; lanes mask the applications.
+// curand_init(seed, slot, 0) for every slot < n (render.h:84-92).  Each lane owns kInitChunk
+// consecutive slots: one seed scramble + subsequence jump A^(first * 2^67) applied digit by digit
+// in base 4 (as skipahead_sequence; the digit position's matrix is wave-uniform, lanes mask the
+// applications), then one mat-vec with A^(2^67) per following slot (state(s+1) = A^(2^67) state(s)).
+constexpr int kInitChunk = 16;
 __global__ __launch_bounds__(kBlock) void init_states_kernel(uint4* states, long long n, uint64_t seed,
                                                             const uint32_t* __restrict__ seq, int digits) {
-  const long long slot = (long long)blockIdx.x * kBlock + threadIdx.x;
-  const bool live = slot < n;
+  const long long first = ((long long)blockIdx.x * kBlock + threadIdx.x) * kInitChunk;
+  if (first >= n) return;
   rtx::State st = rtx::seed_state(seed);
-  unsigned long long x = live ? (unsigned long long)slot : 0ull;
+  unsigned long long x = (unsigned long long)first;
   for (int d = 0; d < digits; ++d) {
     const unsigned dig = (unsigned)(x & 3u);
     x >>= 2;
@@ -954,7 +956,13 @@ __global__ __launch_bounds__(kBlock) void init_states_kernel(uint4* states, long
       }
     }
   }
-  if (live) {
+  for (int c = 0; c < kInitChunk && first + c < n; ++c) {
+    if (c > 0) {
+      uint32_t out[5];
+      rtx::mat_apply(seq, st.v, out);
+      for (int k = 0; k < 5; ++k) st.v[k] = out[k];
+    }
+    const long long slot = first + c;
     states[2 * slot] = make_uint4(st.d, st.v[0], st.v[1], st.v[2]);
     states[2 * slot + 1] = make_uint4(st.v[3], st.v[4], 0u, 0u);
   }
@@ -1393,7 +1401,8 @@ int rt_render_init(rt_ctx* c, int32_t width, int32_t height, uint64_t seed) {
   }
   int digits = 0;
   for (unsigned long long x = (unsigned long long)(n - 1); x; x >>= 2) ++digits;
-  const long long blocks = (n + kBlock - 1) / kBlock;
+  const long long lanes = (n + kInitChunk - 1) / kInitChunk;
+  const long long blocks = (lanes + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(init_states_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, c->states, n, seed,
                      (const uint32_t*)c->seq, digits);
   HIPCHK(c, hipGetLastError());
@@ -1489,6 +1498,20 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
 }
 
 float rt_last_render_ms(const rt_ctx* c) { return c ? c->last_ms : 0.0f; }
+
+int rt_read_states(rt_ctx* c, int64_t first, int64_t count, uint32_t* out) {
+  if (!c || !out || first < 0 || count < 0) return fail(c, RT_ERR_ARG, "bad read_states args");
+  if (!c->states || first + count > c->states_n) return fail(c, RT_ERR_STATE, "states not initialised");
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<uint4> tmp((size_t)count * 2);
+  HIPCHK(c, hipMemcpy(tmp.data(), c->states + 2 * first, tmp.size() * sizeof(uint4), hipMemcpyDeviceToHost));
+  for (int64_t k = 0; k < count; ++k) {
+    const uint4 a = tmp[2 * k], b = tmp[2 * k + 1];
+    const uint32_t w[6] = {a.x, a.y, a.z, a.w, b.x, b.y};
+    memcpy(out + 6 * k, w, sizeof(w));
+  }
+  return RT_OK;
+}
 
 int rt_audit_log(rt_ctx* c, float* out, int32_t cap) {
   if (!c) return -1;

@@ -163,3 +163,21 @@ def test_against_committed_golden(rtlib, gpu_ctx, key, scene, W, H, spp, fbs, de
     out = torch.zeros(H * W * 3, dtype=torch.uint8, device="cuda")
     gpu_ctx.resolve(args, fb.data_ptr(), out.data_ptr())
     assert np.array_equal(out.cpu().numpy().reshape(H, W, 3)[::-1], g[f"{key}_png"])
+
+
+def test_render_init_states_match_curand_init(rtlib, gpu_ctx, oracle):
+    """rt_render_init == curand_init(1984, slot, 0) for every slot class: chunk starts, chunk
+    interiors, the last slot, and the golden subsequences of tests/golden/xorwow_uniforms.json."""
+    import json
+    import os
+
+    W, H = 1200, 800
+    gpu_ctx.render_init(W, H, 1984)
+    rng = np.random.default_rng(7)
+    slots = sorted(set([0, 1, 2, 15, 16, 17, 1023, 959999, W * H - 1] + list(rng.integers(0, W * H, 200))))
+    for s in slots:
+        got = gpu_ctx.read_states(int(s), 1)[0]
+        assert np.array_equal(got, oracle.xorwow_init(1984, int(s), 0)), s
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "xorwow_uniforms.json")))
+    for s, words in gold["states"].items():
+        assert np.array_equal(gpu_ctx.read_states(int(s), 1)[0], np.array(words, np.uint32))
