@@ -75,6 +75,7 @@ struct DScene {
   const rt_perlin* perlins;
   const rt_image* images;
   const uint8_t* texels;
+  const float2* pmargin; // per prim: reference-chain safety margins (see bvh_closest)
   float* dbg;            // audit log (F_CHECK): 16 floats per disagreeing BVH query
   unsigned* dbg_n;
   int32_t dbg_cap;
@@ -508,12 +509,25 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
       return pe >= 0;
     }
     if (best_prim < 0) return false;
-    for (int kr = last0 + (best_rank >> 1);; kr = (kr - 1) >> 1) {
-      if constexpr ((F & F_STATS) != 0) ++nnode;
-      const float4 lo = nodes_of<F>(S)[2 * (base + kr)], hi = nodes_of<F>(S)[2 * (base + kr) + 1];
-      if (!box_hit(lo, hi, r, inv, tmin, tmax)) {
-        if constexpr ((F & F_STATS) != 0) ++nfall;
-        return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
+    // Reference ancestors whose box contains the winner's box with a margin wider than any
+    // displacement of its computed hit point (hit-distance error up to ~4e-4 t for grazing
+    // spheres, slab rounding 2^-22 of the distance) cannot reject this ray, so only the other
+    // chain positions are tested.  pmargin = {bitmask of chain positions with margin < 0.05,
+    // smallest margin among the rest} (computed at upload).
+    const float2 pm = S.pmargin[best_prim];
+    const float dmax = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)),
+                                       __builtin_fabsf(r.d.z));
+    const float bound = 0.001953125f * best * dmax;  // 2^-9 * t * |d|_inf
+    const unsigned must = bound < pm.y ? __float_as_uint(pm.x) : 0xffffffffu;
+    int pos = 0;
+    for (int kr = last0 + (best_rank >> 1);; kr = (kr - 1) >> 1, ++pos) {
+      if ((must >> pos) & 1u) {
+        if constexpr ((F & F_STATS) != 0) ++nnode;
+        const float4 lo = nodes_of<F>(S)[2 * (base + kr)], hi = nodes_of<F>(S)[2 * (base + kr) + 1];
+        if (!box_hit(lo, hi, r, inv, tmin, tmax)) {
+          if constexpr ((F & F_STATS) != 0) ++nfall;
+          return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
+        }
       }
       if (kr == 0) return true;
     }
@@ -706,9 +720,8 @@ template <int F>
 __device__ V tex_value(const DScene& S, int ti, float u, float v, V p) {
   const rt_texture T = S.texs[ti];
   if constexpr ((F & F_CHECKER) != 0) {
-    if (T.type == RT_TEX_CHECKER) {  // texture.h:37-45
-      const float s = rtm::det_sinf(10.0f * p.x) * rtm::det_sinf(10.0f * p.y) * rtm::det_sinf(10.0f * p.z);
-      return tex_leaf<F>(S, S.texs[s < 0 ? T.b : T.a], u, v, p);
+    if (T.type == RT_TEX_CHECKER) {  // texture.h:37-45: sin(10x) sin(10y) sin(10z) < 0 -> odd
+      return tex_leaf<F>(S, S.texs[rtm::checker_odd(10.0f * p.x, 10.0f * p.y, 10.0f * p.z) ? T.b : T.a], u, v, p);
     }
   }
   return tex_leaf<F>(S, T, u, v, p);
@@ -1210,7 +1223,7 @@ struct SahBuilder {
 };
 
 int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<rt_prim>& prims,
-                         std::vector<rt_bvh_node>& nodes) {
+                         std::vector<rt_bvh_node>& nodes, std::vector<float2>& pmargin) {
   const int inner = (1 << rows) - 1, last0 = (1 << (rows - 1)) - 1;
   std::vector<int> members;
   for (int k = last0; k < inner; ++k) {
@@ -1229,6 +1242,30 @@ int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<
   const float t0 = s->camera.time0, t1 = s->camera.time1;
   std::vector<rth::Box> box(s->n_prims);
   for (int id : members) box[id] = rth::prim_box(prims[id], s->triangles, t0 < t1 ? t0 : t1, t0 < t1 ? t1 : t0);
+  // Safety margins of each primitive's reference chain: margin of chain position j = smallest
+  // distance from the primitive's box (over the camera shutter) to the faces of its j-th
+  // reference ancestor (position 0 = its last-row node).  Stored as {bitmask of positions with
+  // margin < 0.05 (always tested), smallest margin of the other positions}.
+  for (int k = last0; k < inner; ++k) {
+    const rt_bvh_node& nd = s->nodes[base + k];
+    for (int id : {nd.leaf_a, nd.leaf_b}) {
+      if (id < 0) continue;
+      uint32_t mask = 0;
+      float safe = INFINITY;
+      int pos = 0;
+      for (int a = k;; a = (a - 1) >> 1, ++pos) {
+        const rt_bvh_node& an = s->nodes[base + a];
+        float mm = INFINITY;
+        for (int q = 0; q < 3; ++q) mm = std::min(mm, std::min(box[id].lo[q] - an.lo[q], an.hi[q] - box[id].hi[q]));
+        if (!(mm >= 0.05f)) mask |= 1u << pos;
+        else safe = std::min(safe, mm);
+        if (a == 0) break;
+      }
+      float mbits;
+      memcpy(&mbits, &mask, 4);
+      pmargin[id] = make_float2(mbits, safe);
+    }
+  }
   const int fb = (int)nodes.size();
   nodes.resize(fb + 2);  // record 0 = root
   SahBuilder sb{box, nodes, fb};
@@ -1327,7 +1364,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
     if (s->world[k] < 0 || s->world[k] >= s->n_objects) return fail(c, RT_ERR_SCENE, "world index out of range");
   for (int k = 0; k < s->n_objects; ++k) {
     const rt_object& o = s->objects[k];
-    if (o.kind == RT_OBJ_BVH && (o.b < 2 || o.a < 0 || o.a + (1 << o.b) - 1 > s->n_nodes))
+    if (o.kind == RT_OBJ_BVH && (o.b < 2 || o.b > 30 || o.a < 0 || o.a + (1 << o.b) - 1 > s->n_nodes))
       return fail(c, RT_ERR_SCENE, "bvh out of range");
     if ((o.kind == RT_OBJ_PRIM || o.kind == RT_OBJ_LIST) && (o.a < 0 || o.a + (o.kind == RT_OBJ_LIST ? o.b : 1) > s->n_prims))
       return fail(c, RT_ERR_SCENE, "prim index out of range");
@@ -1349,10 +1386,11 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   }
   std::vector<rt_bvh_node> nodes(s->nodes, s->nodes + s->n_nodes);
   std::vector<rt_object> objects(s->objects, s->objects + s->n_objects);
+  std::vector<float2> pmargin(s->n_prims, make_float2(-INFINITY, -INFINITY));
   for (rt_object& o : objects) {
     o.c = -1;
     if (o.kind == RT_OBJ_BVH) {
-      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes);
+      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes, pmargin);
       if (fast < 0) return fail(c, RT_ERR_SCENE, "malformed reference bvh");
       o.c = fast;
     }
@@ -1369,6 +1407,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   if ((rc = upload(c, s->triangles, (size_t)s->n_triangles, &d.tris))) return rc;
   if ((rc = upload(c, nodes.data(), nodes.size(), &dn))) return rc;
   if ((rc = upload(c, s->materials, (size_t)s->n_materials, &dm))) return rc;
+  if ((rc = upload(c, pmargin.data(), pmargin.size(), &d.pmargin))) return rc;
   if ((rc = upload(c, s->textures, (size_t)s->n_textures, &d.texs))) return rc;
   if ((rc = upload(c, s->perlins, (size_t)s->n_perlins, &d.perlins))) return rc;
   if ((rc = upload(c, s->images, (size_t)s->n_images, &d.images))) return rc;
