@@ -37,7 +37,8 @@
 #include "rt_xorwow.h"
 
 #define RT_PRIM_TYPE_MASK 0xff
-#define RT_PRIM_FLAG_UV 0x100  // material needs sphere u,v (image texture)
+#define RT_PRIM_FLAG_UV 0x100      // material needs sphere u,v (image texture)
+#define RT_PRIM_FLAG_UNIT_T 0x200  // moving sphere with time0 = 0, time1 - time0 = 1
 
 // Scene feature mask: the render kernel is instantiated per feature set so that a scene pays
 // registers only for the primitive / object / texture kinds it contains.
@@ -153,21 +154,27 @@ using Rng = rtx::State;
 // vec3.h:129-141 (left-to-right argument order).
 __device__ __forceinline__ float urange(Rng& s, float lo, float hi) { return lo + (hi - lo) * rtx::uniform(s); }
 __device__ V in_unit_sphere(Rng& s) {
-  for (;;) {
+  V p;
+  bool inside;
+  do {
     const float a = urange(s, -1.0f, 1.0f);
     const float b = urange(s, -1.0f, 1.0f);
     const float c = urange(s, -1.0f, 1.0f);
-    const V p = mk(a, b, c);
-    if (len2(p) < 1.0f) return p;
-  }
+    p = mk(a, b, c);
+    inside = len2(p) < 1.0f;
+  } while (!inside);
+  return p;
 }
 __device__ V in_unit_disk(Rng& s) {
-  for (;;) {
+  V p;
+  bool inside;
+  do {
     const float a = urange(s, -1.0f, 1.0f);
     const float b = urange(s, -1.0f, 1.0f);
-    const V p = mk(a, b, 0.0f);
-    if (len2(p) < 1.0f) return p;
-  }
+    p = mk(a, b, 0.0f);
+    inside = len2(p) < 1.0f;
+  } while (!inside);
+  return p;
 }
 
 // ------------------------------------------------------------------ primitive tests (t only)
@@ -194,8 +201,11 @@ __device__ __forceinline__ bool sphere_t(const Ray& r, V c, float rad, float tmi
   t = root;
   return true;
 }
+// moving_sphere::center (moving_sphere.h:20-22).  With time0 = 0 and time1 - time0 = 1 (flag
+// set at upload) (tm - 0) / 1 is exactly tm, so the division is skipped.
 __device__ __forceinline__ V moving_center(const PrimRec& q, float tm) {
-  return mk(q.a.x, q.a.y, q.a.z) + ((tm - q.b.w) / q.c.x) * mk(q.b.x, q.b.y, q.b.z);
+  const float sc = (__float_as_int(q.c.z) & RT_PRIM_FLAG_UNIT_T) ? tm : (tm - q.b.w) / q.c.x;
+  return mk(q.a.x, q.a.y, q.a.z) + sc * mk(q.b.x, q.b.y, q.b.z);
 }
 // Rect axis layout: normal axis ax, in-plane axes (ia, ib).
 __device__ __forceinline__ void rect_axes(int type, int& ax, int& ia, int& ib) {
@@ -732,58 +742,63 @@ __device__ V tex_value(const DScene& S, int ti, float u, float v, V p) {
 template <int F>
 __device__ bool scatter(const DScene& S, const Ray& in, const Hit& h, V& att, Ray& out, V& em, Rng& rng) {
   const int4 m = S.mats[h.mat];
+  const int mt = m.x;
   em = mk(0.0f, 0.0f, 0.0f);
-  switch (m.x) {
-    case RT_MAT_LAMBERTIAN: {
-      V dir = h.n + unit(in_unit_sphere(rng));
+  // lambertian, metal and isotropic each draw exactly one random_in_unit_sphere and nothing else
+  // (material.h:26,52,135): one shared rejection loop keeps every lane's draw order and lets
+  // the wave run a single loop instead of one per material.
+  V sp = mk(0.0f, 0.0f, 0.0f);
+  if (mt == RT_MAT_LAMBERTIAN || mt == RT_MAT_METAL || mt == RT_MAT_ISOTROPIC) sp = in_unit_sphere(rng);
+  if (mt == RT_MAT_DIELECTRIC) {  // material.h:64-104
+    att = mk(1.0f, 1.0f, 1.0f);
+    const float ir = __int_as_float(m.z);
+    const float ratio = h.front ? (1.0f / ir) : ir;
+    const V ud = unit(in.d);
+    const float c = __builtin_fminf(dot(neg(ud), h.n), 1.0f);
+    const float sn = __builtin_sqrtf(1.0f - c * c);
+    V dir;
+    bool refl = ratio * sn > 1.0f;
+    if (!refl) {
+      const float sr = (1.0f - ratio) / (1.0f + ratio);
+      const float r0 = sr * sr;
+      const float rf = r0 + (1.0f - r0) * rtm::det_pow5f(1.0f - c);
+      refl = rf > rtx::uniform(rng);
+    }
+    if (refl) {
+      dir = ud - (2.0f * dot(ud, h.n)) * h.n;
+    } else {  // vec3.h:152-158
+      const float ct = __builtin_fminf(dot(neg(ud), h.n), 1.0f);
+      const V perp = ratio * (ud + ct * h.n);
+      const V par = (-__builtin_sqrtf(__builtin_fabsf(1.0f - len2(perp)))) * h.n;
+      dir = perp + par;
+    }
+    out = Ray{h.p, dir, in.tm};
+    return true;
+  }
+  const V tex = tex_value<F>(S, m.y, h.u, h.v, h.p);  // albedo, or emission for diffuse_light
+  switch (mt) {
+    case RT_MAT_LAMBERTIAN: {  // material.h:25-35
+      V dir = h.n + unit(sp);
       const float e = 1e-6f;
       if (__builtin_fabsf(dir.x) < e && __builtin_fabsf(dir.y) < e && __builtin_fabsf(dir.z) < e) dir = h.n;
       out = Ray{h.p, dir, in.tm};
-      att = tex_value<F>(S, m.y, h.u, h.v, h.p);
+      att = tex;
       return true;
     }
-    case RT_MAT_METAL: {
+    case RT_MAT_METAL: {  // material.h:50-55
       const V ud = unit(in.d);
       const V refl = ud - (2.0f * dot(ud, h.n)) * h.n;
-      const float fuzz = __int_as_float(m.z);
-      out = Ray{h.p, refl + fuzz * in_unit_sphere(rng), in.tm};
-      att = tex_value<F>(S, m.y, h.u, h.v, h.p);
+      out = Ray{h.p, refl + __int_as_float(m.z) * sp, in.tm};
+      att = tex;
       return dot(out.d, h.n) > 0;
     }
-    case RT_MAT_DIELECTRIC: {
-      att = mk(1.0f, 1.0f, 1.0f);
-      const float ir = __int_as_float(m.z);
-      const float ratio = h.front ? (1.0f / ir) : ir;
-      const V ud = unit(in.d);
-      const float c = __builtin_fminf(dot(neg(ud), h.n), 1.0f);
-      const float sn = __builtin_sqrtf(1.0f - c * c);
-      V dir;
-      bool refl = ratio * sn > 1.0f;
-      if (!refl) {
-        const float sr = (1.0f - ratio) / (1.0f + ratio);
-        const float r0 = sr * sr;
-        const float rf = r0 + (1.0f - r0) * rtm::det_pow5f(1.0f - c);
-        refl = rf > rtx::uniform(rng);
-      }
-      if (refl) {
-        dir = ud - (2.0f * dot(ud, h.n)) * h.n;
-      } else {  // vec3.h:152-158
-        const float ct = __builtin_fminf(dot(neg(ud), h.n), 1.0f);
-        const V perp = ratio * (ud + ct * h.n);
-        const V par = (-__builtin_sqrtf(__builtin_fabsf(1.0f - len2(perp)))) * h.n;
-        dir = perp + par;
-      }
-      out = Ray{h.p, dir, in.tm};
-      return true;
-    }
-    case RT_MAT_DIFFUSE_LIGHT:
-      em = tex_value<F>(S, m.y, h.u, h.v, h.p);
+    case RT_MAT_DIFFUSE_LIGHT:  // material.h:115-121
+      em = tex;
       return false;
-    default: {  // isotropic
-      out = Ray{h.p, in_unit_sphere(rng), in.tm};
-      att = tex_value<F>(S, m.y, h.u, h.v, h.p);
+    default:  // isotropic, material.h:133-137
+      out = Ray{h.p, sp, in.tm};
+      att = tex;
       return true;
-    }
   }
 }
 
@@ -1048,10 +1063,11 @@ const Variant kVariants[] = {
     RT_VARIANT(F_SPHERES | F_LDS),
     RT_VARIANT(F_ALL | F_LDS),
     RT_VARIANT(F_CORNELL),
+    RT_VARIANT(F_CORNELL | F_EXACT),
     RT_VARIANT(F_CORNELL | F_EXACT | F_STATS),
 };
 #undef RT_VARIANT
-constexpr int kNumVariants = 14;
+constexpr int kNumVariants = 15;
 constexpr int kLdsBudget = 156 * 1024;  // bytes of staged nodes + primitives + stacks per workgroup
 
 // Smallest compiled variant that covers the scene's features and the requested mode.
@@ -1067,11 +1083,11 @@ int pick_variant(int features, bool stats, bool exact, bool check, bool lds) {
     }
     return best;
   };
-  if (lds && mode == 0) {
-    const int v = best_of(F_LDS);
-    if (v >= 0) return v;
-  }
-  return best_of(mode);
+  const int v = best_of(mode);
+  if (v >= 0 && lds && mode == 0)  // the LDS twin of that variant, when one is compiled
+    for (int w = 0; w < kNumVariants; ++w)
+      if (kVariants[w].mask == (kVariants[v].mask | F_LDS)) return w;
+  return v;
 }
 int variant_block(int v) { return (kVariants[v].mask & F_LDS) != 0 ? 1024 : 256; }
 
@@ -1381,6 +1397,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   for (rt_prim& p : prims) {
     const rt_material& m = s->materials[p.material];
     if (p.type == RT_PRIM_SPHERE && m.type != RT_MAT_DIELECTRIC && tex_needs_uv(s, m.texture)) p.type |= RT_PRIM_FLAG_UV;
+    if (p.type == RT_PRIM_MOVING_SPHERE && p.p[7] == 0.0f && p.p[8] == 1.0f) p.type |= RT_PRIM_FLAG_UNIT_T;
     int32_t none = -1;
     memcpy(&p.p[9], &none, 4);
   }

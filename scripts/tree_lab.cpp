@@ -282,7 +282,20 @@ int main(int argc, char** argv) {
     run(nm, T, md);
     if (leaf == 1) {
       Stats st;
-      for (const Ray& r : rays) trace_inline(T, r, st);
+      std::vector<int> hist(256, 0);
+      double wave_max = 0, wave_sum = 0;
+      int lane = 0, cur_max = 0;
+      for (const Ray& r : rays) {
+        Stats one;
+        trace_inline(T, r, one);
+        st.box += one.box; st.prim += one.prim; st.steps += one.steps; st.maxstack = std::max(st.maxstack, one.maxstack);
+        hist[std::min(255, (int)one.steps)]++;
+        cur_max = std::max(cur_max, (int)one.steps);
+        if (++lane == 64) { wave_max += cur_max; wave_sum += 1; lane = 0; cur_max = 0; }
+      }
+      long long acc = 0; int p50=0,p90=0,p99=0;
+      for (int i = 0; i < 256; ++i) { acc += hist[i]; if (!p50 && acc >= 0.5*nr) p50=i; if (!p90 && acc >= 0.9*nr) p90=i; if (!p99 && acc >= 0.99*nr) p99=i; }
+      printf("steps p50 %d p90 %d p99 %d; mean over consecutive 64-ray groups of max steps: %.1f\n", p50, p90, p99, wave_max / wave_sum);
       printf("%-18s nodes %4zu depth %2d | per ray: box %6.2f prim %5.2f steps %5.2f maxstack %2.0f\n",
              "sah1-inline-prims", T.nodes.size(), md, st.box / nr, st.prim / nr, st.steps / nr, st.maxstack);
     }
