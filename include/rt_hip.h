@@ -167,6 +167,8 @@ enum rt_cam_mode {
 #define RT_FLAG_NO_LDS 4          /* keep the scene in global memory even when it fits in LDS   */
 #define RT_FLAG_AUDIT 2           /* run both traversals per BVH query, keep the exact result and
                                      log every disagreement (read back with rt_audit_log)       */
+#define RT_FLAG_WIDEST 8          /* testing: run the widest compiled kernel variant that covers
+                                     the scene instead of the narrowest (same pixels)           */
 
 typedef struct rt_render_args {
   int32_t width, height;  /* full image size; N = width*height drives the RNG slots (H3)  */

@@ -23,13 +23,14 @@ from dataclasses import dataclass
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "librt_hip.so")
+LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(_PKG, "librt_hip.so")  # override: experiments
 
 RT_CAM_REF_SLOT0 = 0
 RT_CAM_PER_PIXEL = 1
 RT_FLAG_EXACT_TRAVERSAL = 1
 RT_FLAG_AUDIT = 2
 RT_FLAG_NO_LDS = 4
+RT_FLAG_WIDEST = 8
 
 PRIM_SPHERE, PRIM_MOVING_SPHERE, PRIM_RECT_XY, PRIM_RECT_XZ, PRIM_RECT_YZ, PRIM_TRIANGLE = range(6)
 OBJ_PRIM, OBJ_LIST, OBJ_BVH, OBJ_XFORM, OBJ_MEDIUM = range(5)
@@ -224,8 +225,9 @@ def scene(name: str) -> Scene:
 def make_args(width: int, height: int, spp: int, fb_first: int = 0, fb_count: int = 1, max_depth: int = 50,
               cam_mode: int = RT_CAM_REF_SLOT0, band_rows: int = 0, band_first: int = 0, band_stride: int = 1,
               stats: bool = False, seed: int = 1984, exact: bool = False, audit: bool = False,
-              lds: bool = True) -> rt_render_args:
+              lds: bool = True, widest: bool = False) -> rt_render_args:
     flags = (RT_FLAG_EXACT_TRAVERSAL if exact else 0) | (RT_FLAG_AUDIT if audit else 0) | (0 if lds else RT_FLAG_NO_LDS)
+    flags |= RT_FLAG_WIDEST if widest else 0
     return rt_render_args(width, height, spp, fb_first, fb_count, max_depth, cam_mode,
                           band_rows if band_rows > 0 else height, band_first, band_stride,
                           1 if stats else 0, flags, seed)

@@ -776,30 +776,27 @@ __device__ bool scatter(const DScene& S, const Ray& in, const Hit& h, V& att, Ra
     return true;
   }
   const V tex = tex_value<F>(S, m.y, h.u, h.v, h.p);  // albedo, or emission for diffuse_light
-  switch (mt) {
-    case RT_MAT_LAMBERTIAN: {  // material.h:25-35
-      V dir = h.n + unit(sp);
-      const float e = 1e-6f;
-      if (__builtin_fabsf(dir.x) < e && __builtin_fabsf(dir.y) < e && __builtin_fabsf(dir.z) < e) dir = h.n;
-      out = Ray{h.p, dir, in.tm};
-      att = tex;
-      return true;
-    }
-    case RT_MAT_METAL: {  // material.h:50-55
-      const V ud = unit(in.d);
-      const V refl = ud - (2.0f * dot(ud, h.n)) * h.n;
-      out = Ray{h.p, refl + __int_as_float(m.z) * sp, in.tm};
-      att = tex;
-      return dot(out.d, h.n) > 0;
-    }
-    case RT_MAT_DIFFUSE_LIGHT:  // material.h:115-121
-      em = tex;
-      return false;
-    default:  // isotropic, material.h:133-137
-      out = Ray{h.p, sp, in.tm};
-      att = tex;
-      return true;
+  if (mt == RT_MAT_DIFFUSE_LIGHT) {  // material.h:115-121
+    em = tex;
+    return false;
   }
+  // The other materials differ only in the scattered direction; one Ray write after the
+  // selection (a per-case struct store was miscompiled in the widest kernel variant: origin
+  // x/y taken from the incoming ray, see scripts/diag_trace.py).
+  V dir = sp;  // isotropic, material.h:133-137
+  bool cont = true;
+  if (mt == RT_MAT_LAMBERTIAN) {  // material.h:25-35
+    dir = h.n + unit(sp);
+    const float e = 1e-6f;
+    if (__builtin_fabsf(dir.x) < e && __builtin_fabsf(dir.y) < e && __builtin_fabsf(dir.z) < e) dir = h.n;
+  } else if (mt == RT_MAT_METAL) {  // material.h:50-55
+    const V ud = unit(in.d);
+    dir = (ud - (2.0f * dot(ud, h.n)) * h.n) + __int_as_float(m.z) * sp;
+    cont = dot(dir, h.n) > 0;
+  }
+  out = Ray{h.p, dir, in.tm};
+  att = tex;
+  return cont;
 }
 
 // ------------------------------------------------------------------ kernels
@@ -815,6 +812,10 @@ struct RenderParams {
   int W, H, rows, spp, fb_first, max_depth, cam_mode, pad;
   int pad3, pad4;
   uint32_t cam_state[6];
+#ifdef RT_TRACE
+  float* trace;
+  long long trace_item;
+#endif
 };
 
 constexpr int kBlock = 256;
@@ -886,59 +887,76 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
       }
     }
     if (__ballot(item >= 0) == 0) break;
-    if (item < 0) continue;
-
-    // ---- begin a sample: jitter + camera ray (render.h:105-108, camera.h:49-58)
-    if (depth == 0) {
-      if (s == 0) {
-        cam.d = P.cam_state[0];
-        for (int k = 0; k < 5; ++k) cam.v[k] = P.cam_state[1 + k];
+    if (item >= 0) {  // idle lanes wait at the loop head (no divergent continue)
+      // ---- begin a sample: jitter + camera ray (render.h:105-108, camera.h:49-58)
+      if (depth == 0) {
+        if (s == 0) {
+          cam.d = P.cam_state[0];
+          for (int k = 0; k < 5; ++k) cam.v[k] = P.cam_state[1 + k];
+        }
+        const float u = ((float)i + rtx::uniform(loc)) / (float)P.W;
+        const float v = ((float)j + rtx::uniform(loc)) / (float)P.H;
+        Rng& cr = per_pixel ? loc : cam;
+        const V rd = C.lens_radius * in_unit_disk(cr);
+        const V off = rd.x * ld3(C.u) + rd.y * ld3(C.v);
+        ray.o = ld3(C.origin) + off;
+        ray.d = ld3(C.lower_left) + u * ld3(C.horizontal) + v * ld3(C.vertical) - ld3(C.origin) - off;
+        ray.tm = urange(cr, C.time0, C.time1);
+        att = mk(1.0f, 1.0f, 1.0f);
       }
-      const float u = ((float)i + rtx::uniform(loc)) / (float)P.W;
-      const float v = ((float)j + rtx::uniform(loc)) / (float)P.H;
-      Rng& cr = per_pixel ? loc : cam;
-      const V rd = C.lens_radius * in_unit_disk(cr);
-      const V off = rd.x * ld3(C.u) + rd.y * ld3(C.v);
-      ray.o = ld3(C.origin) + off;
-      ray.d = ld3(C.lower_left) + u * ld3(C.horizontal) + v * ld3(C.vertical) - ld3(C.origin) - off;
-      ray.tm = urange(cr, C.time0, C.time1);
-      att = mk(1.0f, 1.0f, 1.0f);
-    }
 
-    // ---- one segment (render.h:60-77)
-    ++nseg;
-    Hit h;
-    bool ended = false;
-    V contrib;
-    if (!world_hit<F>(S, ray, h, loc, nnode, nprim, nfall)) {
-      contrib = att * ld3(S.bg);
-      ended = true;
-    } else {
-      V a, em;
-      Ray sc;
-      if (scatter<F>(S, ray, h, a, sc, em, loc)) {
-        att = att * a;
-        ray = sc;
-        if (++depth == P.max_depth) {
-          contrib = mk(0.0f, 0.0f, 0.0f);
+      // ---- one segment (render.h:60-77)
+      ++nseg;
+      Hit h;
+      bool ended = false;
+      V contrib;
+  #ifdef RT_TRACE
+      const Ray ray_in = ray;
+      const unsigned rng_in = loc.d;
+  #endif
+      const bool hit_any = world_hit<F>(S, ray, h, loc, nnode, nprim, nfall);
+  #ifdef RT_TRACE
+      if (item == P.trace_item && P.trace) {
+        const unsigned k = atomicAdd((unsigned*)P.trace, 1u);
+        if (k < 255) {
+          float* e = P.trace + 16 * (k + 1);
+          e[0] = ray_in.o.x; e[1] = ray_in.o.y; e[2] = ray_in.o.z; e[3] = ray_in.d.x; e[4] = ray_in.d.y;
+          e[5] = ray_in.d.z; e[6] = ray_in.tm; e[7] = hit_any ? h.t : -1.0f; e[8] = __int_as_float(hit_any ? h.mat : -1);
+          e[9] = h.p.x; e[10] = h.p.y; e[11] = h.p.z; e[12] = __uint_as_float(rng_in); e[13] = __uint_as_float(loc.d);
+          e[14] = __int_as_float(s); e[15] = __int_as_float(depth);
+        }
+      }
+  #endif
+      if (!hit_any) {
+        contrib = att * ld3(S.bg);
+        ended = true;
+      } else {
+        V a, em;
+        Ray sc;
+        if (scatter<F>(S, ray, h, a, sc, em, loc)) {
+          att = att * a;
+          ray = sc;
+          if (++depth == P.max_depth) {
+            contrib = mk(0.0f, 0.0f, 0.0f);
+            ended = true;
+          }
+        } else {
+          contrib = att * em;
           ended = true;
         }
-      } else {
-        contrib = att * em;
-        ended = true;
       }
-    }
-    if (ended) {
-      col = col + contrib;
-      depth = 0;
-      ++nsamp;
-      if (++s == P.spp) {
-        const V out = (1.0f / (float)P.spp) * col;
-        float* dst = P.fb + 3 * (((long long)f * P.rows + r) * P.W + i);
-        dst[0] = out.x;
-        dst[1] = out.y;
-        dst[2] = out.z;
-        item = -1;
+      if (ended) {
+        col = col + contrib;
+        depth = 0;
+        ++nsamp;
+        if (++s == P.spp) {
+          const V out = (1.0f / (float)P.spp) * col;
+          float* dst = P.fb + 3 * (((long long)f * P.rows + r) * P.W + i);
+          dst[0] = out.x;
+          dst[1] = out.y;
+          dst[2] = out.z;
+          item = -1;
+        }
       }
     }
   }
@@ -1071,15 +1089,16 @@ constexpr int kNumVariants = 15;
 constexpr int kLdsBudget = 156 * 1024;  // bytes of staged nodes + primitives + stacks per workgroup
 
 // Smallest compiled variant that covers the scene's features and the requested mode.
-int pick_variant(int features, bool stats, bool exact, bool check, bool lds) {
+int pick_variant(int features, bool stats, bool exact, bool check, bool lds, bool widest = false) {
   const int modes = F_STATS | F_EXACT | F_CHECK | F_LDS;
   const int mode = check ? F_CHECK : ((stats ? F_STATS : 0) | (exact ? F_EXACT : 0));
-  auto best_of = [&](int want) {  // covering variant with the fewest feature bits
+  auto best_of = [&](int want) {  // covering variant with the fewest (widest: most) feature bits
     int best = -1;
     for (int v = 0; v < kNumVariants; ++v) {
       const int m = kVariants[v].mask;
       if ((m & modes) != want || (features & ~m) != 0) continue;
-      if (best < 0 || __builtin_popcount(m) < __builtin_popcount(kVariants[best].mask)) best = v;
+      const int pm = __builtin_popcount(m), pb = best < 0 ? 0 : __builtin_popcount(kVariants[best].mask);
+      if (best < 0 || (widest ? pm > pb : pm < pb)) best = v;
     }
     return best;
   };
@@ -1513,7 +1532,8 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   const bool check = (a->flags & RT_FLAG_AUDIT) != 0;
   const size_t lds_bytes = (size_t)(2 * c->dev_nodes + 3 * c->dev_prims) * sizeof(float4);
   const bool use_lds = lds_bytes + 1024 * kStackDepth * 4 <= (size_t)kLdsBudget && (a->flags & RT_FLAG_NO_LDS) == 0;
-  const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds);
+  const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
+                               (a->flags & RT_FLAG_WIDEST) != 0);
   if (check) {
     if (!c->dbg) {
       HIPCHK(c, hipMalloc((void**)&c->dbg, 16 * sizeof(float) * kAuditCap + 64));
@@ -1533,6 +1553,13 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   const long long need = (long long)((P.total_items + bs - 1) / bs);
   const unsigned blocks = (unsigned)std::max(1LL, std::min(resident, need));
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+#ifdef RT_TRACE
+  static float* tbuf = nullptr;
+  if (!tbuf) hipMalloc((void**)&tbuf, 16 * 256 * sizeof(float));
+  hipMemsetAsync(tbuf, 0, 16 * 256 * sizeof(float), c->stream);
+  P.trace = getenv("RT_TRACE_ITEM") ? tbuf : nullptr;
+  P.trace_item = getenv("RT_TRACE_ITEM") ? atoll(getenv("RT_TRACE_ITEM")) : -1;
+#endif
   void* kargs[] = {&P};
   HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), kargs, shmem, c->stream));
   HIPCHK(c, hipGetLastError());
@@ -1548,6 +1575,15 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
     counters->samples = host_cnt[4];
     counters->fallbacks = host_cnt[5];
   }
+#ifdef RT_TRACE
+  if (P.trace) {
+    std::vector<float> hb(16 * 256);
+    hipMemcpy(hb.data(), tbuf, hb.size() * sizeof(float), hipMemcpyDeviceToHost);
+    FILE* fo = fopen(getenv("RT_TRACE_OUT"), "wb");
+    fwrite(hb.data(), sizeof(float), hb.size(), fo);
+    fclose(fo);
+  }
+#endif
   if (host_cnt[4] != (unsigned long long)a->spp * P.total_items)
     return fail(c, RT_ERR_HIP, "render kernel did not complete every sample");
   return RT_OK;

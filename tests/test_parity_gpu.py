@@ -63,6 +63,32 @@ def test_small_bit_exact(rtlib, gpu_ctx, oracle, scene, W, H, spp, fb_first, fb_
     assert cnt["samples"] == W * H * spp * fb_count
 
 
+VARIANT_MODES = [  # every compiled kernel family, forced to its widest variant (RT_FLAG_WIDEST)
+    ("culled", {}), ("culled_global", {"lds": False}), ("exact", {"exact": True}),
+    ("stats", {"stats": True}), ("exact_stats", {"exact": True, "stats": True}), ("audit", {"audit": True}),
+]
+
+
+@pytest.mark.parametrize("scene,W,H,spp,fb_first,fb_count,cam", SMALL)
+def test_widest_variants_bit_exact(rtlib, gpu_ctx, oracle, scene, W, H, spp, fb_first, fb_count, cam):
+    """The catch-all kernel variants must give the same pixels as the narrow ones a scene gets."""
+    import torch
+
+    ref = oracle.RefScene(scene)
+    want = [ref.render(W, H, spp, fb_first + f, 50, cam)[0].reshape(H, W, 3) for f in range(fb_count)]
+    gpu_ctx.upload(rtlib.Scene.builtin(scene))
+    gpu_ctx.render_init(W, H, 1984)
+    bad = []
+    for name, kw in VARIANT_MODES:
+        fb = torch.zeros(fb_count * H * W * 3, dtype=torch.float32, device="cuda")
+        gpu_ctx.render(rtlib.make_args(W, H, spp, fb_first, fb_count, 50, cam, widest=True, **kw), fb.data_ptr())
+        got = fb.cpu().numpy().reshape(fb_count, H, W, 3)
+        n = sum(int((_bits(got[f]) != _bits(want[f])).any(axis=2).sum()) for f in range(fb_count))
+        if n:
+            bad.append(f"{name}: {n} pixels")
+    assert not bad, f"{scene}: " + ", ".join(bad)
+
+
 def test_resolve_matches_average_images(rtlib, gpu_ctx, oracle):
     import torch
 
