@@ -28,6 +28,22 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
 NODE_BYTES = 32         # rt_bvh_node
 PRIM_BYTES = 48         # rt_prim
 ITEM_BYTES = 32 + 12    # per (fb, pixel): RNG state read + fb write
+VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 4  # wave64 VALU instructions/s: 1024 SIMDs, 4 cycles each
+
+
+def committed_pmc(workload: str):
+    """PMC summary (scripts/profile.sh + scripts/pmc_summary.py) committed for this exact workload."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "*_pmc.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload and "hbm_bytes_per_launch" in d:
+            best = (os.path.relpath(f, ROOT), d)
+    return best
 
 
 def parse():
@@ -157,6 +173,9 @@ def main():
     if rank == 0:
         avg_ms = sum(kms) / len(kms)
         roof = None
+        workload = (f"C2 {a.scene} {a.width}x{a.height}, {a.nfb} fb x {a.spp} spp = {a.nfb * a.spp} rays/pixel, "
+                    f"depth {a.depth}, cam {a.cam}, traversal {'exact' if a.exact else 'culled'}"
+                    f"{'' if not a.no_lds else ', global scene'}")
         if stats is not None:
             items = a.nfb * len(rows) * a.width
             bytes_launch = NODE_BYTES * stats["node_tests"] + PRIM_BYTES * stats["prim_tests"] + ITEM_BYTES * items
@@ -169,14 +188,25 @@ def main():
                     "node_tests_per_segment": round(stats["node_tests"] / max(stats["segments"], 1), 3),
                     "prim_tests_per_segment": round(stats["prim_tests"] / max(stats["segments"], 1), 3),
                     "fallbacks": stats["fallbacks"]}
+            pmc = committed_pmc(workload) if world == 1 else None
+            if pmc is not None:
+                src, d = pmc
+                # measured HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, gfx950 correction)
+                roof["traffic"] = d["hbm_bytes_per_launch"]
+                roof["traffic_source"] = src
+                if "SQ_INSTS_VALU" in d:
+                    t_issue = d["SQ_INSTS_VALU"] / VALU_ISSUE_PER_S
+                    roof["valu"] = {"insts_per_launch": int(d["SQ_INSTS_VALU"]),
+                                    "issue_time_ms": round(t_issue * 1e3, 3),
+                                    "issue_frac": round(t_issue / (avg_ms * 1e-3), 4),
+                                    "lane_utilisation": round(d.get("valu_lane_utilisation", float("nan")), 4),
+                                    "source": src}
         out = {
             "metric": "Mrays/sec (primary+bounces) on RTIOW random-spheres 1200x800x100spp",
             "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (reference scene generator, seed 1984)",
-            "config": {"workload": f"C2 {a.scene} {a.width}x{a.height}, {a.nfb} fb x {a.spp} spp = "
-                                   f"{a.nfb * a.spp} rays/pixel, depth {a.depth}, cam {a.cam}, "
-                                   f"traversal {'exact' if a.exact else 'culled'}",
+            "config": {"workload": workload,
                        "scene": a.scene, "width": a.width, "height": a.height, "rays_per_pixel": a.nfb * a.spp,
                        "no_fb": a.nfb, "spp_per_fb": a.spp, "max_depth": a.depth,
                        "segments_per_step": int(segs), "parallelism": f"rows{world}"},
