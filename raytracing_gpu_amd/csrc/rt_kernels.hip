@@ -117,6 +117,29 @@ __device__ __forceinline__ int* stack_of(const DScene& S) {
 // (entry d of thread t at [d * block + t]) so a wave's pushes/pops hit 64 distinct banks.
 constexpr int kStackDepth = 16;
 
+// Diagnostic build only (-DRT_STAMPS): per-wave cycle shares of the render loop's phases
+// (s_memtime stamps, cdna_hip_programming.md section 7).  Phase = code run after the stamp.
+#ifdef RT_STAMPS
+constexpr int kStampPhases = 8;  // head, camera, world glue, node tests, prim tests, validation, scatter, one stamp
+__shared__ unsigned long long rt_stamp_acc[16][kStampPhases + 2];
+__device__ __forceinline__ void rt_stamp(int ph) {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long act = __ballot(1);
+  if ((int)__lane_id() == __ffsll((long long)act) - 1) {
+    unsigned long long* a = rt_stamp_acc[threadIdx.x >> 6];
+    if (a[0] != 0) a[2 + a[1]] += t - a[0];
+    a[0] = t;
+    a[1] = (unsigned long long)ph;
+  }
+}
+#define RT_STAMP(ph) rt_stamp(ph)
+#else
+#define RT_STAMP(ph)
+#endif
+
 struct V {
   float x, y, z;
 };
@@ -456,6 +479,7 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
     int sp = 0, cur = 0;
     bool overflow = false;
     for (;;) {
+      RT_STAMP(3);
       const float4* n = nodes_of<F>(S) + 2 * (fb + 2 * cur);
       const float4 l0 = n[0], l1 = n[1], r0 = n[2], r1 = n[3];
       if constexpr ((F & F_STATS) != 0) nnode += 2;
@@ -469,6 +493,7 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
       for (int side = 0; side < 2; ++side) {
         const int ch = side == 0 ? c0 : c1;
         if ((side == 0 ? hl : hr) && ch < 0) {
+          RT_STAMP(4);
           const int pi = -ch - 1;
           const PrimRec q = load_prim<F>(S, pi);
           float t;
@@ -481,6 +506,7 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
             }
           }
           if (side == 0) hl = false; else hr = false;
+          RT_STAMP(3);
         }
       }
       if (hl && hr) {
@@ -497,6 +523,7 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
       if (sp == 0) break;
       cur = stk[BS * --sp];
     }
+    RT_STAMP(5);
     if (overflow) {  // a subtree was dropped: answer on the exact visit set instead
       if constexpr ((F & F_STATS) != 0) ++nfall;
       return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
@@ -816,6 +843,9 @@ struct RenderParams {
   float* trace;
   long long trace_item;
 #endif
+#ifdef RT_STAMPS
+  unsigned long long* stamps;
+#endif
 };
 
 constexpr int kBlock = 256;
@@ -842,6 +872,11 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
     __syncthreads();
   }
   const unsigned lane = __lane_id();
+#ifdef RT_STAMPS
+  if (lane < kStampPhases + 2) rt_stamp_acc[threadIdx.x >> 6][lane] = 0;
+  __syncthreads();
+  RT_STAMP(0);
+#endif
   long long item = -1;  // -1: idle
   bool done = false;
   int f = 0, i = 0, r = 0, j = 0, s = 0, depth = 0;
@@ -855,6 +890,8 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
 
   for (;;) {
     // ---- refill idle lanes (one atomic per wave, ballot-compacted ranks)
+    RT_STAMP(7);  // back-to-back pair: phase 7 = the cost of one stamp per loop trip
+    RT_STAMP(0);
     const unsigned long long idle = __ballot(item < 0 && !done);
     const unsigned long long busy = __ballot(item >= 0);
     const int nidle = __popcll(idle);
@@ -890,6 +927,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
     if (item >= 0) {  // idle lanes wait at the loop head (no divergent continue)
       // ---- begin a sample: jitter + camera ray (render.h:105-108, camera.h:49-58)
       if (depth == 0) {
+        RT_STAMP(1);
         if (s == 0) {
           cam.d = P.cam_state[0];
           for (int k = 0; k < 5; ++k) cam.v[k] = P.cam_state[1 + k];
@@ -914,7 +952,9 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
       const Ray ray_in = ray;
       const unsigned rng_in = loc.d;
   #endif
+      RT_STAMP(2);
       const bool hit_any = world_hit<F>(S, ray, h, loc, nnode, nprim, nfall);
+      RT_STAMP(6);
   #ifdef RT_TRACE
       if (item == P.trace_item && P.trace) {
         const unsigned k = atomicAdd((unsigned*)P.trace, 1u);
@@ -961,6 +1001,10 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
     }
   }
 
+#ifdef RT_STAMPS
+  RT_STAMP(0);
+  if (lane < kStampPhases) atomicAdd(P.stamps + lane, rt_stamp_acc[threadIdx.x >> 6][2 + lane]);
+#endif
   const unsigned long long ws = wave_sum(nseg), wm = wave_sum(nsamp);
   unsigned long long wn = 0, wp = 0, wf = 0;
   if constexpr ((F & F_STATS) != 0) {
@@ -1553,6 +1597,12 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   const long long need = (long long)((P.total_items + bs - 1) / bs);
   const unsigned blocks = (unsigned)std::max(1LL, std::min(resident, need));
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+#ifdef RT_STAMPS
+  static unsigned long long* sbuf = nullptr;
+  if (!sbuf) hipMalloc((void**)&sbuf, 8 * sizeof(unsigned long long));
+  hipMemsetAsync(sbuf, 0, 8 * sizeof(unsigned long long), c->stream);
+  P.stamps = sbuf;
+#endif
 #ifdef RT_TRACE
   static float* tbuf = nullptr;
   if (!tbuf) hipMalloc((void**)&tbuf, 16 * 256 * sizeof(float));
@@ -1575,6 +1625,15 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
     counters->samples = host_cnt[4];
     counters->fallbacks = host_cnt[5];
   }
+#ifdef RT_STAMPS
+  if (getenv("RT_STAMPS_OUT")) {
+    unsigned long long hs[8];
+    hipMemcpy(hs, sbuf, sizeof(hs), hipMemcpyDeviceToHost);
+    FILE* fo = fopen(getenv("RT_STAMPS_OUT"), "ab");
+    fwrite(hs, sizeof(hs), 1, fo);
+    fclose(fo);
+  }
+#endif
 #ifdef RT_TRACE
   if (P.trace) {
     std::vector<float> hb(16 * 256);
