@@ -233,12 +233,42 @@ int rt_draw(rt_ctx* ctx, const rt_render_args* args, uint8_t* png_rgb_host, rt_c
 
 /* ------------------------------------------------------------------ host scene library */
 /* Builds one of the reference scenes (scenes.h) on the host: "basic", "first", "big1" (alias
- * "random"), "two_spheres", "two_perlin", "cornell", "cornell_smoke".  The returned handle owns
- * the arrays its rt_scene_soa points at. */
+ * "random"), "two_spheres", "two_perlin", "cornell", "cornell_smoke", "triangle", "triangles",
+ * "backpack" (renders only its ground, H17).  The returned handle owns the arrays its
+ * rt_scene_soa points at. */
 typedef struct rt_scene_host rt_scene_host;
 int rt_scene_build(const char* name, rt_scene_host** out);
 const rt_scene_soa* rt_scene_view(const rt_scene_host* s);
 void rt_scene_free(rt_scene_host* s);
+
+/* Decoded image, the stbi_load layout make_image() uploads (texture.h:166-203): rows top to
+ * bottom, bytes_per_pixel interleaved channels. */
+typedef struct rt_image_asset {
+  int32_t width, height, bytes_per_pixel;
+  int32_t pad;
+  const uint8_t* data;
+} rt_image_asset;
+/* One mesh as create_meshes_d() builds it (triangle_mesh.h:147-204): 24 floats per triangle,
+ * v0[3] v1[3] v2[3] n0[3] n1[3] n2[3] u0 v0 u1 v1 u2 v2.  vertex_normals = 0 uses the face
+ * normal (triangle.h:166); image = index into the assets' images for its lambertian texture. */
+typedef struct rt_mesh_asset {
+  int32_t n_triangles;
+  int32_t vertex_normals;
+  int32_t image;
+  int32_t pad;
+  const float* data;
+} rt_mesh_asset;
+typedef struct rt_scene_assets {
+  int32_t n_images;
+  int32_t n_meshes;
+  const rt_image_asset* images;
+  const rt_mesh_asset* meshes;
+} rt_scene_assets;
+/* rt_scene_build with external assets (the files the reference reads at scene construction):
+ * "earth" (images[0] = earthmap, scenes.h:278-320), "door" / "cup" (meshes[0] with its texture,
+ * scenes.h:478-523,576-621), "final" (the composed book-2 final scene of config C5: images[0]
+ * and meshes[0]), and every name rt_scene_build accepts (assets may be NULL). */
+int rt_scene_build_ex(const char* name, const rt_scene_assets* assets, rt_scene_host** out);
 
 #ifdef __cplusplus
 }

@@ -348,6 +348,27 @@ struct MarbleTex : Texture {  // texture.h:80-91
 };
 
 // ---------------------------------------------------------------- materials (material.h)
+struct ImageTex : Texture {  // texture.h:125-163 (decoded texels owned here)
+  std::vector<uint8_t> data;
+  int w = 0, h = 0, bpp = 0;
+  ImageTex(const uint8_t* d, int ww, int hh, int bb) : w(ww), h(hh), bpp(bb) {
+    if (d && ww > 0 && hh > 0) data.assign(d, d + (size_t)ww * hh * bb);
+  }
+  V3 value(float u, float v, const V3&) const override {
+    if (data.empty()) return V3(0, 1, 1);  // texture.h:146-147
+    const float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);  // clamp_d, common.h:62-67
+    const float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+    const double vv = 1.0 - vc;  // double (texture.h:150)
+    int i = (int)(uu * w);       // float * int -> float
+    int j = (int)(vv * h);       // double * int -> double
+    if (i >= w) i = w - 1;
+    if (j >= h) j = h - 1;
+    const float cs = 1.0f / 255.0f;
+    const uint8_t* px = data.data() + (size_t)j * (bpp * w) + (size_t)i * bpp;
+    return V3(cs * px[0], cs * px[1], cs * px[2]);
+  }
+};
+
 struct Material {
   virtual bool scatter(const Ray& in, const Rec& r, V3& att, Ray& out, Draw& g) const = 0;
   virtual V3 emitted(float, float, const V3&) const { return V3(0, 0, 0); }
@@ -526,6 +547,79 @@ struct Rect : Hittable {
     return true;
   }
 };
+struct Triangle : Hittable {  // triangle.h:6-178
+  V3 p0, p1, p2, e0, e1, n0, n1, n2;
+  float uv[6];
+  float d00, d01, d11, inv;
+  bool vn = false;
+  const Material* m;
+  Triangle(V3 a, V3 b, V3 c, const float* tuv, const V3* n, const Material* mm) : p0(a), p1(b), p2(c), m(mm) {
+    for (int k = 0; k < 6; ++k) uv[k] = tuv[k];
+    e0 = p1 - p0;  // "v0", "v1" of triangle.h:26-27
+    e1 = p2 - p0;
+    d00 = dot(e0, e0);
+    d01 = dot(e0, e1);
+    d11 = dot(e1, e1);
+    inv = 1.0f / (d00 * d11 - d01 * d01);
+    if (n) {
+      n0 = n[0];
+      n1 = n[1];
+      n2 = n[2];
+      vn = true;
+    }
+  }
+  bool hit(const Ray& r, float tmin, float tmax, Rec& rec, Draw&) const override {  // :120-178
+    const float eps = 0.0000001f;
+    const V3 hh = cross(r.d, e1);
+    const float a = dot(e0, hh);
+    if (a > -eps && a < eps) return false;
+    const float f = 1.0f / a;
+    const V3 sv = r.o - p0;
+    const float u = f * dot(sv, hh);
+    if (u < 0.0f || u > 1.0f) return false;
+    const V3 q = cross(sv, e0);
+    const float v = f * dot(r.d, q);
+    if ((v < 0.0f) | (u + v > 1.0f)) return false;
+    const float t = f * dot(e1, q);
+    if (t < tmin || t > tmax || t < eps) return false;
+    rec.t = t;
+    rec.m = m;
+    rec.p = r.at(t);
+    const V3 v2 = rec.p - p0;
+    const float d20 = dot(v2, e0), d21 = dot(v2, e1);
+    const float b0 = (d11 * d20 - d01 * d21) * inv;
+    const float b1 = (d00 * d21 - d01 * d20) * inv;
+    const float b2 = 1.0f - b0 - b1;
+    rec.u = b2 * uv[0] + b0 * uv[2] + b1 * uv[4];
+    rec.v = b2 * uv[1] + b0 * uv[3] + b1 * uv[5];
+    if (!vn) {
+      rec.face(r, cross(e1, e0));  // unnormalised face normal (H12)
+    } else {
+      const V3 nn(b2 * n0.x + b0 * n1.x + b1 * n2.x, b2 * n0.y + b0 * n1.y + b1 * n2.y,
+                  b2 * n0.z + b0 * n1.z + b1 * n2.z);
+      rec.face(r, nn);
+    }
+    return true;
+  }
+  bool bbox(float, float, Box& o) const override {  // :46-98, flat extents padded by 1e-4
+    const V3 vs[3] = {p0, p1, p2};
+    for (int k = 0; k < 3; ++k) {
+      float lo = vs[0][k], hi = vs[0][k];
+      for (int q = 1; q < 3; ++q) {
+        if (vs[q][k] < lo) lo = vs[q][k];
+        if (vs[q][k] > hi) hi = vs[q][k];
+      }
+      if (std::fabs(lo - hi) < 0.000001f) {
+        hi += 0.0001f;
+        lo -= 0.0001f;
+      }
+      o.lo[k] = lo;
+      o.hi[k] = hi;
+    }
+    return true;
+  }
+};
+
 struct List : Hittable {
   bool is_prim() const override { return false; }  // hittable_list.h:23-59 (later object wins ties)
   std::vector<const Hittable*> objs;
@@ -958,6 +1052,71 @@ static void build_cornell(ref_scene& s, bool smoke) {  // scenes.h:323-404
   s.cam = Camera(V3(278, 278, -800), V3(278, 278, 0), V3(0, 1, 0), 40, 1.0f, 0.0f, 10.0f, 0, 1);
 }
 
+// triangle_scene, scenes.h:409-428.
+static void build_triangle(ref_scene& s) {
+  s.background = kSky;
+  const float uv[6] = {0, 0, 0, 1, 1, 0};
+  s.world = s.list({s.H<Triangle>(V3(-0.5f, 0, 0), V3(0, 1, 10), V3(0.0f, 0, 0), uv, nullptr, s.lam(V3(0, 1, 0))),
+                    s.H<Sphere>(V3(0, -100.5f, -1), 100.0f, s.lam(V3(0, 0, 1)))});
+  s.cam = Camera(V3(0, 0, -3), V3(0, 0, 0), V3(0, 1, 0), 40, 16.0f / 9.0f, 0.0f, 10.0f, 0, 1);
+}
+// triangles_scene, scenes.h:432-475: triangle_mesh = bvh_node over 4 triangles (world_init state).
+static void build_triangles(ref_scene& s, Draw& g) {
+  s.background = kSky;
+  const float uv[6] = {0, 0, 0, 1, 1, 0};
+  std::vector<const Hittable*> t = {
+      s.H<Triangle>(V3(-0.5f, 0, 0), V3(0, 1, 10), V3(0.5f, 0, 0), uv, nullptr, s.lam(V3(0, 1, 0))),
+      s.H<Triangle>(V3(0.5f, 0, 0), V3(0, 1, 10), V3(0.5f, 1, 0), uv, nullptr, s.lam(V3(1, 1, 0))),
+      s.H<Triangle>(V3(1.5f, 0, 0), V3(0, 2, 10), V3(1.5f, 1, 0), uv, nullptr, s.lam(V3(1, 1, 1))),
+      s.H<Triangle>(V3(1.5f, 0, 0), V3(1.5f, 1, 10), V3(1.5f, 0, 2), uv, nullptr, s.lam(V3(1, 1, 1)))};
+  s.world = s.list({s.H<RefBvh>(t, 0.0f, 1.0f, g), s.H<Sphere>(V3(0, -100.5f, -1), 100.0f, s.lam(V3(0, 0, 1)))});
+  s.cam = Camera(V3(0, 0, -3), V3(0, 0, 0), V3(0, 1, 0), 40, 16.0f / 9.0f, 0.0f, 10.0f, 0, 1);
+}
+// earth_scene, scenes.h:278-320.
+static bool build_earth(ref_scene& s, const ref_assets* a) {
+  if (!a || a->n_images < 1) return false;
+  s.background = kBlack;
+  const ref_image& im = a->images[0];
+  auto* tex = s.X<ImageTex>(im.data, im.width, im.height, im.bytes_per_pixel);
+  s.world = s.list({s.H<Sphere>(V3(0, 0, 0), 2.0f, s.M<Lambert>(tex)),
+                    s.H<Rect>(2, -5.0f, 5.0f, -3.0f, 3.0f, 6.0f, s.M<Light>(s.X<Solid>(V3(4.0f, 4.0f, 4.0f))))});
+  s.cam = Camera(V3(13.0f, 0.0f, 3.0f), V3(0.0f, 0.0f, 0.0f), V3(0, 1, 0), 20, 16.0f / 9.0f, 0.1f, 10.0f, 0, 1);
+  return true;
+}
+// One triangle_mesh of create_meshes_d (triangle_mesh.h:147-204): lambertian(image_texture).
+static const Hittable* build_mesh(ref_scene& s, const ref_assets* a, const ref_mesh& m, Draw& g) {
+  const Texture* tex;
+  if (m.image >= 0 && m.image < a->n_images) {
+    const ref_image& im = a->images[m.image];
+    tex = s.X<ImageTex>(im.data, im.width, im.height, im.bytes_per_pixel);
+  } else {
+    tex = s.X<ImageTex>(nullptr, 0, 0, 0);
+  }
+  const Material* mat = s.M<Lambert>(tex);
+  std::vector<const Hittable*> t;
+  for (int k = 0; k < m.n_triangles; ++k) {
+    const float* d = m.data + 24 * (size_t)k;
+    const V3 n[3] = {V3(d[9], d[10], d[11]), V3(d[12], d[13], d[14]), V3(d[15], d[16], d[17])};
+    t.push_back(s.H<Triangle>(V3(d[0], d[1], d[2]), V3(d[3], d[4], d[5]), V3(d[6], d[7], d[8]), d + 18,
+                              m.vertex_normals ? n : nullptr, mat));
+  }
+  return s.H<RefBvh>(t, 0.0f, 1.0f, g);
+}
+// door_scene / cup_scene, scenes.h:478-523,576-621.
+static bool build_mesh_scene(ref_scene& s, const ref_assets* a, Draw& g, V3 from, V3 at) {
+  if (!a || a->n_meshes < 1 || !a->meshes[0].data || a->meshes[0].n_triangles < 3) return false;
+  s.background = kSky;
+  s.world = s.list({build_mesh(s, a, a->meshes[0], g), s.H<Sphere>(V3(0, -100, -1), 100.0f, s.lam(V3(0, 1, 0)))});
+  s.cam = Camera(from, at, V3(0, 1, 0), 20, 16.0f / 9.0f, 0.0f, 10.0f, 0, 1);
+  return true;
+}
+// backpack_scene, scenes.h:526-572: only the ground sphere remains (H17).
+static void build_backpack(ref_scene& s) {
+  s.background = kSky;
+  s.world = s.list({s.H<Sphere>(V3(0, -100, -1), 100.0f, s.lam(V3(0, 1, 0)))});
+  s.cam = Camera(V3(0, 0, -3), V3(0, 0, 0), V3(0, 1, 0), 20, 16.0f / 9.0f, 0.0f, 10.0f, 0, 1);
+}
+
 // ---------------------------------------------------------------- integrator (render.h:55-113)
 static V3 trace(const ref_scene& s, Ray r, Draw& g, int depth) {
   V3 att(1, 1, 1);
@@ -1011,7 +1170,7 @@ static void render_pixel(const ref_scene& s, int i, int j, int W, int H, int spp
 // ---------------------------------------------------------------- C API
 extern "C" {
 
-int ref_scene_create(const char* name, int rtl, ref_scene** out) {
+int ref_scene_create_ex(const char* name, int rtl, const ref_assets* a, ref_scene** out) {
   std::unique_ptr<ref_scene> s(new ref_scene);
   s->name = name;
   Rng st = rng_init(1984, 0, 0);  // world_init  scenes.h:28-32
@@ -1025,11 +1184,18 @@ int ref_scene_create(const char* name, int rtl, ref_scene** out) {
   else if (n == "two_perlin") build_two_perlin(*s, g);
   else if (n == "cornell") build_cornell(*s, false);
   else if (n == "cornell_smoke") build_cornell(*s, true);
+  else if (n == "triangle") build_triangle(*s);
+  else if (n == "triangles") build_triangles(*s, g);
+  else if (n == "backpack") build_backpack(*s);
+  else if (n == "earth") { if (!build_earth(*s, a)) return 1; }
+  else if (n == "door") { if (!build_mesh_scene(*s, a, g, V3(-3, 4, -5), V3(0, 1, 0))) return 1; }
+  else if (n == "cup") { if (!build_mesh_scene(*s, a, g, V3(0, 0, -1), V3(0, 0, 0))) return 1; }
   else return 1;
   s->h20 = tl_h20;
   *out = s.release();
   return 0;
 }
+int ref_scene_create(const char* name, int rtl, ref_scene** out) { return ref_scene_create_ex(name, rtl, nullptr, out); }
 void ref_scene_destroy(ref_scene* s) { delete s; }
 long long ref_capture_rays(float* buf, long long max_rays) {  // buf = NULL stops capturing
   const long long n = g_cap_n.exchange(0);

@@ -25,6 +25,12 @@ enum { REF_CAM_REF_SLOT0 = 0, REF_CAM_PER_PIXEL = 1 };
 /* Build one of the reference's scenes (scenes.h).  rtl != 0 evaluates multi-draw argument lists
  * right-to-left instead of left-to-right (hazard H9; used only for the layout pin test). */
 int ref_scene_create(const char* name, int rtl, ref_scene** out);
+/* Scenes that read files in the reference take decoded assets: "earth" (images[0]), "door" /
+ * "cup" (meshes[0], 24 floats per triangle: v0 v1 v2 n0 n1 n2 u0 v0 u1 v1 u2 v2). */
+typedef struct ref_image { int width, height, bytes_per_pixel, pad; const uint8_t* data; } ref_image;
+typedef struct ref_mesh { int n_triangles, vertex_normals, image, pad; const float* data; } ref_mesh;
+typedef struct ref_assets { int n_images, n_meshes; const ref_image* images; const ref_mesh* meshes; } ref_assets;
+int ref_scene_create_ex(const char* name, int rtl, const ref_assets* assets, ref_scene** out);
 void ref_scene_destroy(ref_scene* s);
 /* Capture world-query rays (8 floats: o, d, time, 0) into buf during later ref_render calls
  * (design experiments only); returns the number captured since the previous call. */

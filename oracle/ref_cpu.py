@@ -36,6 +36,7 @@ def lib() -> ctypes.CDLL:
             raise RuntimeError(f"{LIB_PATH} missing: run `make -C oracle`")
         L = ctypes.CDLL(LIB_PATH)
         L.ref_scene_create.argtypes = [ctypes.c_char_p, c_int, POINTER(c_void_p)]
+        L.ref_scene_create_ex.argtypes = [ctypes.c_char_p, c_int, c_void_p, POINTER(c_void_p)]
         L.ref_scene_destroy.argtypes = [c_void_p]
         L.ref_scene_aspect.argtypes = [c_void_p]
         L.ref_scene_aspect.restype = c_float
@@ -57,12 +58,41 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
+class _Image(ctypes.Structure):
+    _fields_ = [("width", c_int), ("height", c_int), ("bytes_per_pixel", c_int), ("pad", c_int),
+                ("data", c_void_p)]
+
+
+class _Mesh(ctypes.Structure):
+    _fields_ = [("n_triangles", c_int), ("vertex_normals", c_int), ("image", c_int), ("pad", c_int),
+                ("data", c_void_p)]
+
+
+class _Assets(ctypes.Structure):
+    _fields_ = [("n_images", c_int), ("n_meshes", c_int), ("images", POINTER(_Image)), ("meshes", POINTER(_Mesh))]
+
+
 class RefScene:
-    def __init__(self, name: str, rtl: bool = False):
+    def __init__(self, name: str, rtl: bool = False, images=None, meshes=None):
+        """images: HxWxC uint8 arrays; meshes: (tris (n, 24) float32, vertex_normals, image index)."""
         self.name = name
         self._h = c_void_p()
-        if lib().ref_scene_create(name.encode(), 1 if rtl else 0, ctypes.byref(self._h)) != 0:
-            raise ValueError(f"unknown oracle scene {name!r}")
+        if images is None and meshes is None:
+            rc = lib().ref_scene_create(name.encode(), 1 if rtl else 0, ctypes.byref(self._h))
+        else:
+            imgs = [np.ascontiguousarray(i, np.uint8) for i in (images or [])]
+            imgs = [i[:, :, None] if i.ndim == 2 else i for i in imgs]
+            ms = [(np.ascontiguousarray(t, np.float32).reshape(-1, 24), vn, im) for t, vn, im in (meshes or [])]
+            ia = (_Image * max(len(imgs), 1))()
+            for k, im in enumerate(imgs):
+                ia[k] = _Image(im.shape[1], im.shape[0], im.shape[2], 0, im.ctypes.data)
+            ma = (_Mesh * max(len(ms), 1))()
+            for k, (t, vn, im) in enumerate(ms):
+                ma[k] = _Mesh(t.shape[0], 1 if vn else 0, im, 0, t.ctypes.data)
+            a = _Assets(len(imgs), len(ms), ia, ma)
+            rc = lib().ref_scene_create_ex(name.encode(), 1 if rtl else 0, ctypes.byref(a), ctypes.byref(self._h))
+        if rc != 0:
+            raise ValueError(f"unknown oracle scene {name!r} (or missing assets)")
 
     @property
     def aspect(self) -> float:

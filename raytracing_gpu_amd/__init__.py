@@ -111,6 +111,7 @@ ABI = {
     "rt_resolve": (c_int, [c_void_p, POINTER(rt_render_args), c_void_p, c_void_p]),
     "rt_draw": (c_int, [c_void_p, POINTER(rt_render_args), POINTER(c_uint8), POINTER(rt_counters)]),
     "rt_scene_build": (c_int, [c_char_p, POINTER(c_void_p)]),
+    "rt_scene_build_ex": (c_int, [c_char_p, c_void_p, POINTER(c_void_p)]),
     "rt_scene_view": (POINTER(rt_scene_soa), [c_void_p]),
     "rt_scene_free": (None, [c_void_p]),
 }
@@ -184,9 +185,19 @@ class Scene:
         self.soa = lib().rt_scene_view(self._h).contents
 
     @classmethod
-    def builtin(cls, name: str) -> "Scene":
+    def builtin(cls, name: str, images=None, meshes=None) -> "Scene":
+        """Build a reference scene.  images: HxWxC uint8 arrays (decoded textures, stbi_load layout);
+        meshes: raytracing_gpu_amd.assets.Mesh objects (24 floats per triangle).  Scenes that read
+        files in the reference ("earth", "door", "cup", "final") need them; see assets.py."""
         h = c_void_p()
-        rc = lib().rt_scene_build(name.encode(), ctypes.byref(h))
+        if images is None and meshes is None:
+            rc = lib().rt_scene_build(name.encode(), ctypes.byref(h))
+        else:
+            from .assets import pack_assets
+
+            keep, ptr = pack_assets(images or [], meshes or [])
+            rc = lib().rt_scene_build_ex(name.encode(), ptr, ctypes.byref(h))
+            del keep
         if rc != 0:
             raise RtError(f"rt_scene_build({name!r}) failed with status {rc}")
         return cls(h, name)

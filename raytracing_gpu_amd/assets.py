@@ -1,0 +1,113 @@
+"""Scene assets: decoded images and triangle meshes handed to rt_scene_build_ex.
+
+The reference reads these files while it builds a scene: stbi_load for textures
+(texture.h:166-203, make_image) and assimp for OBJ meshes (triangle_mesh.h:129-352,
+create_meshes).  Here the host decodes them and passes plain arrays through the C ABI:
+
+- `load_image(path)` decodes with Pillow (libjpeg).  The reference uses stb_image v2.26; the two
+  decoders may differ in the last bit of some texels, so texel bytes are "parity unpinned" against
+  the reference's loader (the render of given texels is bit-exact between GPU and oracle).
+- `synthetic_image(w, h)` is a deterministic texture of any shape (tests and benchmarks on a GPU
+  box, where the reference's files do not exist).
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import POINTER, Structure, c_float, c_int32, c_uint8, c_void_p
+
+import numpy as np
+
+TRI_FLOATS = 24  # v0 v1 v2 (9), n0 n1 n2 (9), u0 v0 u1 v1 u2 v2 (6)
+
+
+class rt_image_asset(Structure):
+    _fields_ = [("width", c_int32), ("height", c_int32), ("bytes_per_pixel", c_int32), ("pad", c_int32),
+                ("data", POINTER(c_uint8))]
+
+
+class rt_mesh_asset(Structure):
+    _fields_ = [("n_triangles", c_int32), ("vertex_normals", c_int32), ("image", c_int32), ("pad", c_int32),
+                ("data", POINTER(c_float))]
+
+
+class rt_scene_assets(Structure):
+    _fields_ = [("n_images", c_int32), ("n_meshes", c_int32), ("images", POINTER(rt_image_asset)),
+                ("meshes", POINTER(rt_mesh_asset))]
+
+
+class Mesh:
+    """Triangle soup of one mesh as create_meshes_d builds it: (n, 24) float32 rows."""
+
+    def __init__(self, tris: np.ndarray, vertex_normals: bool = True, image: int = 0, texture_path: str = ""):
+        self.tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, TRI_FLOATS)
+        self.vertex_normals = bool(vertex_normals)
+        self.image = int(image)
+        self.texture_path = texture_path
+
+    def __len__(self) -> int:
+        return self.tris.shape[0]
+
+
+def load_image(path: str) -> np.ndarray:
+    """Decode an image file to HxWxC uint8 (the channel count of the file, like stbi_load(.., 0))."""
+    from PIL import Image
+
+    im = Image.open(path)
+    if im.mode not in ("L", "LA", "RGB", "RGBA"):
+        im = im.convert("RGB")
+    a = np.asarray(im, dtype=np.uint8)
+    return a[:, :, None] if a.ndim == 2 else a
+
+
+def synthetic_image(width: int, height: int, channels: int = 3, seed: int = 1984) -> np.ndarray:
+    """Deterministic test texture: smooth gradients plus a hashed high-frequency component."""
+    y, x = np.mgrid[0:height, 0:width].astype(np.uint32)
+    h = (x * np.uint32(73856093)) ^ (y * np.uint32(19349663)) ^ np.uint32(seed * 83492791 & 0xFFFFFFFF)
+    out = np.empty((height, width, channels), np.uint8)
+    for c in range(channels):
+        g = ((x * (c + 1) * 255) // max(width - 1, 1) + (y * (3 - c) * 255) // max(height - 1, 1)) & 255
+        out[:, :, c] = ((g + ((h >> (8 * c)) & 31)) & 255).astype(np.uint8)
+    return out
+
+
+def pack_assets(images, meshes):
+    """ctypes view of images/meshes; returns (objects to keep alive, pointer to rt_scene_assets)."""
+    imgs = [np.ascontiguousarray(i, dtype=np.uint8) for i in images]
+    imgs = [i[:, :, None] if i.ndim == 2 else i for i in imgs]
+    ia = (rt_image_asset * max(len(imgs), 1))()
+    for k, im in enumerate(imgs):
+        ia[k] = rt_image_asset(im.shape[1], im.shape[0], im.shape[2], 0, im.ctypes.data_as(POINTER(c_uint8)))
+    ma = (rt_mesh_asset * max(len(meshes), 1))()
+    for k, m in enumerate(meshes):
+        ma[k] = rt_mesh_asset(len(m), 1 if m.vertex_normals else 0, m.image, 0, m.tris.ctypes.data_as(POINTER(c_float)))
+    a = rt_scene_assets(len(imgs), len(meshes), ia, ma)
+    keep = (imgs, meshes, ia, ma, a)
+    return keep, ctypes.cast(ctypes.pointer(a), c_void_p)
+
+
+def synthetic_mesh(nu: int = 24, nv: int = 32, image: int = 0) -> Mesh:
+    """Deterministic test mesh near the door scene's look-at point: a wavy sheet of nu x nv quads
+    (two triangles each) with analytic vertex normals and uvs in [0, 1]."""
+    u = np.linspace(0.0, 1.0, nu + 1, dtype=np.float64)
+    v = np.linspace(0.0, 1.0, nv + 1, dtype=np.float64)
+    U, Vv = np.meshgrid(u, v, indexing="ij")
+    X = U - 0.5
+    Y = 2.0 * Vv
+    Z = 0.15 * np.sin(6.0 * U) * np.cos(4.0 * Vv)
+    dzdu = 0.9 * np.cos(6.0 * U) * np.cos(4.0 * Vv)
+    dzdv = -0.6 * np.sin(6.0 * U) * np.sin(4.0 * Vv)
+    # normal = (1, 0, dzdu) x (0, 2, dzdv) normalised
+    N = np.stack([-2.0 * dzdu, -dzdv, 2.0 * np.ones_like(U)], axis=-1)
+    N /= np.linalg.norm(N, axis=-1, keepdims=True)
+    P = np.stack([X, Y, Z], axis=-1)
+    rows = []
+    for i in range(nu):
+        for j in range(nv):
+            q = [(i, j), (i + 1, j), (i + 1, j + 1), (i, j + 1)]
+            for a, b, c in ((0, 1, 2), (0, 2, 3)):
+                ids = (q[a], q[b], q[c])
+                row = [*P[ids[0]], *P[ids[1]], *P[ids[2]], *N[ids[0]], *N[ids[1]], *N[ids[2]]]
+                for k in ids:
+                    row += [U[k], Vv[k]]
+                rows.append(row)
+    return Mesh(np.asarray(rows, np.float32), vertex_normals=True, image=image)

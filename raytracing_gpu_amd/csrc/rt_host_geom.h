@@ -56,8 +56,8 @@ inline Box prim_box(const rt_prim& q, const rt_triangle* tris, float t0, float t
       float v[3][3];
       for (int k = 0; k < 3; ++k) {
         v[0][k] = t.v0[k];
-        v[1][k] = t.v0[k] + t.e0[k];
-        v[2][k] = t.v0[k] + t.e1[k];
+        v[1][k] = t.v1[k];
+        v[2][k] = t.v2[k];
       }
       for (int k = 0; k < 3; ++k) {
         b.lo[k] = std::min({v[0][k], v[1][k], v[2][k]});

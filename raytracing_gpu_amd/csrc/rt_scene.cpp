@@ -123,6 +123,23 @@ struct rt_scene_host {
     return (int)mats.size() - 1;
   }
   int lam(F3 c) { return mat(RT_MAT_LAMBERTIAN, solid(c), 0.0f); }
+  // image_texture over a decoded image (texture.h:125-163); texels appended in upload order.
+  int image_tex(const rt_image_asset& a) {
+    rt_image im{};
+    im.width = a.width;
+    im.height = a.height;
+    im.bytes_per_pixel = a.bytes_per_pixel;
+    im.offset = (int32_t)texels.size();
+    const size_t n = (size_t)a.width * a.height * a.bytes_per_pixel;
+    if (a.data && n) texels.insert(texels.end(), a.data, a.data + n);
+    else im.width = 0;  // no data: the reference's cyan fallback (texture.h:146-147)
+    images.push_back(im);
+    rt_texture t{};
+    t.type = RT_TEX_IMAGE;
+    t.a = (int)images.size() - 1;
+    texs.push_back(t);
+    return (int)texs.size() - 1;
+  }
 
   // ---- primitives / objects
   int prim(int type, int m, std::initializer_list<float> p) {
@@ -138,6 +155,30 @@ struct rt_scene_host {
   int moving(F3 c0, F3 c1, float t0, float t1, float r, int m) {
     const F3 d = sub(c1, c0);
     return prim(RT_PRIM_MOVING_SPHERE, m, {c0.x, c0.y, c0.z, r, d.x, d.y, d.z, t0, t1 - t0});
+  }
+  // triangle.h:19-41: edges, barycentric dot products and 1/denominator precomputed; vertex
+  // normals only with the second constructor (n != nullptr).
+  int tri(F3 a, F3 b, F3 c, const float uv[6], const F3* n, int m) {
+    rt_triangle t{};
+    put(t.v0, a);
+    put(t.v1, b);
+    put(t.v2, c);
+    const F3 e0 = sub(b, a), e1 = sub(c, a);
+    put(t.e0, e0);
+    put(t.e1, e1);
+    t.d00 = dot(e0, e0);
+    t.d01 = dot(e0, e1);
+    t.d11 = dot(e1, e1);
+    t.inv_denom = 1.0f / (t.d00 * t.d11 - t.d01 * t.d01);
+    for (int k = 0; k < 6; ++k) t.uv[k] = uv[k];
+    if (n) {
+      put(t.n0, n[0]);
+      put(t.n1, n[1]);
+      put(t.n2, n[2]);
+      t.vertex_normals = 1;
+    }
+    tris.push_back(t);
+    return prim(RT_PRIM_TRIANGLE, m, {(float)(tris.size() - 1)});
   }
   int rect(int type, float a0, float a1, float b0, float b1, float k, int m) {
     return prim(type, m, {a0, a1, b0, b1, k, a1 - a0, b1 - b0});
@@ -400,28 +441,117 @@ void scene_cornell(rt_scene_host& s, bool smoke) {
   s.camera(mk(278, 278, -800), mk(278, 278, 0), mk(0, 1, 0), 40, 1.0f, 0.0f, 10.0f, 0, 1);
 }
 
+// triangle_scene, scenes.h:409-428: one triangle (face normal) and the ground sphere.
+void scene_triangle(rt_scene_host& s) {
+  set_bg(s, kSky, 16.0f / 9.0f);
+  const float uv[6] = {0, 0, 0, 1, 1, 0};
+  s.world.push_back(s.object(RT_OBJ_PRIM, s.tri(mk(-0.5f, 0, 0), mk(0, 1, 10), mk(0.0f, 0, 0), uv, nullptr,
+                                                s.lam(mk(0, 1, 0))), 0));
+  s.world.push_back(s.object(RT_OBJ_PRIM, s.sphere(mk(0, -100.5f, -1), 100.0f, s.lam(mk(0, 0, 1))), 0));
+  s.camera(mk(0, 0, -3), mk(0, 0, 0), mk(0, 1, 0), 40, 16.0f / 9.0f, 0.0f, 10.0f, 0, 1);
+}
+
+// triangles_scene, scenes.h:432-475: four triangles in a triangle_mesh (a bvh_node built with
+// the world_init state) and the ground sphere.
+void scene_triangles(rt_scene_host& s) {
+  set_bg(s, kSky, 16.0f / 9.0f);
+  SceneRng g;
+  const float uv[6] = {0, 0, 0, 1, 1, 0};
+  const int first = (int)s.prims.size();
+  s.tri(mk(-0.5f, 0, 0), mk(0, 1, 10), mk(0.5f, 0, 0), uv, nullptr, s.lam(mk(0, 1, 0)));
+  s.tri(mk(0.5f, 0, 0), mk(0, 1, 10), mk(0.5f, 1, 0), uv, nullptr, s.lam(mk(1, 1, 0)));
+  s.tri(mk(1.5f, 0, 0), mk(0, 2, 10), mk(1.5f, 1, 0), uv, nullptr, s.lam(mk(1, 1, 1)));
+  s.tri(mk(1.5f, 0, 0), mk(1.5f, 1, 10), mk(1.5f, 0, 2), uv, nullptr, s.lam(mk(1, 1, 1)));
+  s.world.push_back(s.bvh(first, 4, 0.0f, 1.0f, g));
+  s.world.push_back(s.object(RT_OBJ_PRIM, s.sphere(mk(0, -100.5f, -1), 100.0f, s.lam(mk(0, 0, 1))), 0));
+  s.camera(mk(0, 0, -3), mk(0, 0, 0), mk(0, 1, 0), 40, 16.0f / 9.0f, 0.0f, 10.0f, 0, 1);
+}
+
+// earth_scene, scenes.h:278-320: image-textured sphere and an emitting xy_rect, black background.
+bool scene_earth(rt_scene_host& s, const rt_scene_assets* a) {
+  if (!a || a->n_images < 1) return false;
+  set_bg(s, kBlack, 16.0f / 9.0f);
+  const int earth = s.mat(RT_MAT_LAMBERTIAN, s.image_tex(a->images[0]), 0.0f);
+  s.world.push_back(s.object(RT_OBJ_PRIM, s.sphere(mk(0, 0, 0), 2.0f, earth), 0));
+  const int light = s.mat(RT_MAT_DIFFUSE_LIGHT, s.solid(mk(4.0f, 4.0f, 4.0f)), 0);
+  s.world.push_back(s.object(RT_OBJ_PRIM, s.rect(RT_PRIM_RECT_XY, -5, 5, -3, 3, 6, light), 0));
+  s.camera(mk(13.0f, 0.0f, 3.0f), mk(0.0f, 0.0f, 0.0f), mk(0, 1, 0), 20, 16.0f / 9.0f, 0.1f, 10.0f, 0, 1);
+  return true;
+}
+
+// One triangle_mesh of create_meshes_d (triangle_mesh.h:147-204): lambertian(image_texture) on
+// every triangle, a bvh_node over them built with the world_init state (triangle_mesh.h:27-35).
+int add_mesh(rt_scene_host& s, const rt_scene_assets* a, const rt_mesh_asset& m, SceneRng& g) {
+  int tex;
+  if (m.image >= 0 && m.image < a->n_images) tex = s.image_tex(a->images[m.image]);
+  else tex = s.image_tex(rt_image_asset{0, 0, 0, 0, nullptr});
+  const int mat = s.mat(RT_MAT_LAMBERTIAN, tex, 0.0f);
+  const int first = (int)s.prims.size();
+  for (int k = 0; k < m.n_triangles; ++k) {
+    const float* d = m.data + 24 * (size_t)k;
+    const F3 n[3] = {mk(d[9], d[10], d[11]), mk(d[12], d[13], d[14]), mk(d[15], d[16], d[17])};
+    s.tri(mk(d[0], d[1], d[2]), mk(d[3], d[4], d[5]), mk(d[6], d[7], d[8]), d + 18, m.vertex_normals ? n : nullptr,
+          mat);
+  }
+  if (m.n_triangles < 3) return -1;
+  return s.bvh(first, m.n_triangles, 0.0f, 1.0f, g);
+}
+
+// door_scene / cup_scene, scenes.h:478-523,576-621: the mesh and a ground sphere.
+bool scene_mesh(rt_scene_host& s, const rt_scene_assets* a, F3 from, F3 at) {
+  if (!a || a->n_meshes < 1 || !a->meshes[0].data) return false;
+  set_bg(s, kSky, 16.0f / 9.0f);
+  SceneRng g;
+  s.world.push_back(add_mesh(s, a, a->meshes[0], g));
+  s.world.push_back(s.object(RT_OBJ_PRIM, s.sphere(mk(0, -100, -1), 100.0f, s.lam(mk(0, 1, 0))), 0));
+  s.camera(from, at, mk(0, 1, 0), 20, 16.0f / 9.0f, 0.0f, 10.0f, 0, 1);
+  return true;
+}
+
+// backpack_scene, scenes.h:526-572: the mesh is overwritten by the ground sphere (H17), so the
+// world is that sphere alone.
+void scene_backpack(rt_scene_host& s) {
+  set_bg(s, kSky, 16.0f / 9.0f);
+  s.world.push_back(s.object(RT_OBJ_PRIM, s.sphere(mk(0, -100, -1), 100.0f, s.lam(mk(0, 1, 0))), 0));
+  s.camera(mk(0, 0, -3), mk(0, 0, 0), mk(0, 1, 0), 20, 16.0f / 9.0f, 0.0f, 10.0f, 0, 1);
+}
+
+int build_named(rt_scene_host& s, const std::string& n, const rt_scene_assets* a) {
+  if (n == "basic") scene_basic(s);
+  else if (n == "first") scene_first(s);
+  else if (n == "big1" || n == "random") scene_big1(s);
+  else if (n == "two_spheres") scene_two_spheres(s);
+  else if (n == "two_perlin") scene_two_perlin(s);
+  else if (n == "cornell") scene_cornell(s, false);
+  else if (n == "cornell_smoke") scene_cornell(s, true);
+  else if (n == "triangle") scene_triangle(s);
+  else if (n == "triangles") scene_triangles(s);
+  else if (n == "backpack") scene_backpack(s);
+  else if (n == "earth") { if (!scene_earth(s, a)) return RT_ERR_ARG; }
+  else if (n == "door") { if (!scene_mesh(s, a, mk(-3, 4, -5), mk(0, 1, 0))) return RT_ERR_ARG; }
+  else if (n == "cup") { if (!scene_mesh(s, a, mk(0, 0, -1), mk(0, 0, 0))) return RT_ERR_ARG; }
+  else return RT_ERR_ARG;
+  return RT_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
-int rt_scene_build(const char* name, rt_scene_host** out) {
+int rt_scene_build_ex(const char* name, const rt_scene_assets* assets, rt_scene_host** out) {
   if (!name || !out) return RT_ERR_ARG;
+  *out = nullptr;
   std::unique_ptr<rt_scene_host> s(new rt_scene_host);
-  const std::string n(name);
-  if (n == "basic") scene_basic(*s);
-  else if (n == "first") scene_first(*s);
-  else if (n == "big1" || n == "random") scene_big1(*s);
-  else if (n == "two_spheres") scene_two_spheres(*s);
-  else if (n == "two_perlin") scene_two_perlin(*s);
-  else if (n == "cornell") scene_cornell(*s, false);
-  else if (n == "cornell_smoke") scene_cornell(*s, true);
-  else return RT_ERR_ARG;
+  const int rc = build_named(*s, std::string(name), assets);
+  if (rc != RT_OK) return rc;
   for (int32_t w : s->world)
     if (w < 0) return RT_ERR_SCENE;
   s->finish();
   *out = s.release();
   return RT_OK;
 }
+
+int rt_scene_build(const char* name, rt_scene_host** out) { return rt_scene_build_ex(name, nullptr, out); }
 
 const rt_scene_soa* rt_scene_view(const rt_scene_host* s) { return s ? &s->view : nullptr; }
 

@@ -22,6 +22,9 @@ SMALL = [
     ("two_perlin", 64, 36, 2, 0, 2, REF),
     ("cornell", 48, 48, 4, 0, 2, REF),
     ("cornell_smoke", 48, 48, 4, 0, 2, REF),
+    ("triangle", 64, 36, 2, 0, 2, REF),
+    ("triangles", 64, 36, 2, 0, 2, REF),
+    ("backpack", 64, 36, 2, 0, 2, REF),
 ]
 
 
@@ -87,6 +90,40 @@ def test_widest_variants_bit_exact(rtlib, gpu_ctx, oracle, scene, W, H, spp, fb_
         if n:
             bad.append(f"{name}: {n} pixels")
     assert not bad, f"{scene}: " + ", ".join(bad)
+
+
+def _asset_scene(name):
+    """(product images/meshes, oracle images/meshes) for scenes that read files in the reference:
+    synthetic texture/mesh of the real assets' kind (the reference's files are not on a GPU box)."""
+    from raytracing_gpu_amd import assets
+
+    img = assets.synthetic_image(341, 152)
+    if name == "earth":
+        return dict(images=[img]), dict(images=[img])
+    m = assets.synthetic_mesh(24, 32, image=0)
+    return dict(images=[img], meshes=[m]), dict(images=[img], meshes=[(m.tris, m.vertex_normals, m.image)])
+
+
+@pytest.mark.parametrize("exact", [False, True], ids=["culled", "exact"])
+@pytest.mark.parametrize("scene", ["earth", "door"])
+def test_asset_scene_bit_exact(rtlib, gpu_ctx, oracle, scene, exact):
+    import torch
+
+    W, H, spp, nfb = 64, 36, 3, 2
+    pa, oa = _asset_scene(scene)
+    gpu_ctx.upload(rtlib.Scene.builtin(scene, **pa))
+    gpu_ctx.render_init(W, H, 1984)
+    fb = torch.zeros(nfb * H * W * 3, dtype=torch.float32, device="cuda")
+    cnt = gpu_ctx.render(rtlib.make_args(W, H, spp, 0, nfb, 50, REF, exact=exact), fb.data_ptr())
+    got = fb.cpu().numpy().reshape(nfb, H, W, 3)
+    ref = oracle.RefScene(scene, **oa)
+    segs = 0
+    for f in range(nfb):
+        want, c, _ = ref.render(W, H, spp, f, 50, REF)
+        segs += c["segments"]
+        diff = _bits(got[f]) != _bits(want.reshape(H, W, 3))
+        assert not diff.any(), f"{scene} fb {f}: {int(diff.any(axis=2).sum())} pixels differ"
+    assert cnt["segments"] == segs
 
 
 def test_resolve_matches_average_images(rtlib, gpu_ctx, oracle):
