@@ -68,13 +68,33 @@ def parse():
     return ap.parse_args()
 
 
+CONFIG_OF = {"big1": "C2", "random": "C2", "cornell_smoke": "C3", "door": "C4", "final": "C5"}
+
+
+def scene_assets(name: str):
+    """Assets of the scenes that read files in the reference (kwargs for the product scene, kwargs
+    for the oracle).  GPU boxes have no reference files: the door mesh comes from the committed
+    assimp-import fixture (tests/golden/door_assimp.npz), textures are synthetic images of the real
+    files' shapes (earthmap.jpg 3410x1518, Door_C.jpg 2048x2048)."""
+    from raytracing_gpu_amd import assets
+
+    if name == "earth":
+        img = assets.synthetic_image(3410, 1518)
+        return dict(images=[img]), dict(images=[img])
+    if name in ("door", "cup", "final"):
+        m = assets.door_mesh_from_fixture(os.path.join(ROOT, "tests", "golden", "door_assimp.npz"))
+        imgs = [assets.synthetic_image(2048, 2048)] if name != "final" else [assets.synthetic_image(3410, 1518)]
+        return dict(images=imgs, meshes=[m]), dict(images=imgs, meshes=[(m.tris, m.vertex_normals, m.image)])
+    return {}, {}
+
+
 def cpu_baseline(a, budget_s: float) -> dict:
     """The CPU oracle (C++ restatement of the reference render path) on the host's cores, over a
     bounded sample of the same workload: every k-th row, all fbs."""
     from oracle import ref_cpu
 
     threads = max(1, min(16, os.cpu_count() or 1))
-    sc = ref_cpu.RefScene(a.scene)
+    sc = ref_cpu.RefScene(a.scene, **scene_assets(a.scene)[1])
     cam = 0 if a.cam == "ref" else 1
     # calibrate on one row of fb 0
     t0 = time.perf_counter()
@@ -111,7 +131,7 @@ def main():
     dev = torch.device("cuda", local)
 
     ctx = rt.Context(local)
-    sc = rt.Scene.builtin(a.scene)
+    sc = rt.Scene.builtin(a.scene, **scene_assets(a.scene)[0])
     ctx.upload(sc)
     cam = rt.RT_CAM_REF_SLOT0 if a.cam == "ref" else rt.RT_CAM_PER_PIXEL
     args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, band_rows=a.band_rows,
@@ -173,7 +193,7 @@ def main():
     if rank == 0:
         avg_ms = sum(kms) / len(kms)
         roof = None
-        workload = (f"C2 {a.scene} {a.width}x{a.height}, {a.nfb} fb x {a.spp} spp = {a.nfb * a.spp} rays/pixel, "
+        workload = (f"{CONFIG_OF.get(a.scene, 'scene')} {a.scene} {a.width}x{a.height}, {a.nfb} fb x {a.spp} spp = {a.nfb * a.spp} rays/pixel, "
                     f"depth {a.depth}, cam {a.cam}, traversal {'exact' if a.exact else 'culled'}"
                     f"{'' if not a.no_lds else ', global scene'}")
         if stats is not None:

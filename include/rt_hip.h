@@ -270,6 +270,24 @@ typedef struct rt_scene_assets {
  * and meshes[0]), and every name rt_scene_build accepts (assets may be NULL). */
 int rt_scene_build_ex(const char* name, const rt_scene_assets* assets, rt_scene_host** out);
 
+/* OBJ mesh ingestion: create_meshes() (triangle_mesh.h:208-352) with assimp's OBJ import
+ * (ReadFile(Triangulate | GenNormals), processNode order) restated, see csrc/rt_obj.cpp.
+ * RT_OBJ_INDEX_REFERENCE reproduces create_meshes_d's indexing of the concatenated vertex array
+ * with per-mesh local indices; RT_OBJ_INDEX_GLOBAL offsets each mesh's indices. */
+enum { RT_OBJ_INDEX_REFERENCE = 0, RT_OBJ_INDEX_GLOBAL = 1 };
+typedef struct rt_obj_mesh rt_obj_mesh;
+typedef struct rt_obj_info {
+  int32_t n_triangles;   /* rows of `triangles` (rt_mesh_asset layout, 24 floats each)         */
+  int32_t n_meshes;      /* aiMeshes the import produced                                        */
+  int32_t n_vertices;    /* concatenated vertex count                                            */
+  int32_t n_textures;    /* distinct diffuse textures of the used materials (reference needs 1) */
+  const float* triangles;
+  const char* texture;   /* first diffuse texture path (OBJ directory + map_Kd), "" if none     */
+} rt_obj_info;
+int rt_obj_load(const char* path, int32_t index_mode, rt_obj_mesh** out);
+const rt_obj_info* rt_obj_view(const rt_obj_mesh* m);
+void rt_obj_free(rt_obj_mesh* m);
+
 #ifdef __cplusplus
 }
 #endif

@@ -112,6 +112,9 @@ ABI = {
     "rt_draw": (c_int, [c_void_p, POINTER(rt_render_args), POINTER(c_uint8), POINTER(rt_counters)]),
     "rt_scene_build": (c_int, [c_char_p, POINTER(c_void_p)]),
     "rt_scene_build_ex": (c_int, [c_char_p, c_void_p, POINTER(c_void_p)]),
+    "rt_obj_load": (c_int, [c_char_p, c_int, POINTER(c_void_p)]),
+    "rt_obj_view": (c_void_p, [c_void_p]),
+    "rt_obj_free": (None, [c_void_p]),
     "rt_scene_view": (POINTER(rt_scene_soa), [c_void_p]),
     "rt_scene_free": (None, [c_void_p]),
 }

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librt_hip.so")
 
-HIP_SOURCES = ["rt_kernels.hip", "rt_scene.cpp"]
+HIP_SOURCES = ["rt_kernels.hip", "rt_scene.cpp", "rt_obj.cpp"]
 HIP_DEPS = HIP_SOURCES + ["rt_detmath.h", "rt_xorwow.h", "rt_host_geom.h"]
 # -ffp-contract=off: no FMA contraction anywhere, so every float op rounds like the reference's
 # C++ source and like the CPU oracle; fp32 div/sqrt correctly rounded (IEEE) on the device.

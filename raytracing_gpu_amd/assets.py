@@ -111,3 +111,61 @@ def synthetic_mesh(nu: int = 24, nv: int = 32, image: int = 0) -> Mesh:
                     row += [U[k], Vv[k]]
                 rows.append(row)
     return Mesh(np.asarray(rows, np.float32), vertex_normals=True, image=image)
+
+
+class rt_obj_info(Structure):
+    _fields_ = [("n_triangles", c_int32), ("n_meshes", c_int32), ("n_vertices", c_int32), ("n_textures", c_int32),
+                ("triangles", POINTER(c_float)), ("texture", ctypes.c_char_p)]
+
+
+OBJ_INDEX_REFERENCE = 0  # create_meshes_d: per-mesh local indices into the concatenated arrays (H16)
+OBJ_INDEX_GLOBAL = 1     # each mesh's indices offset by its first vertex
+
+
+def load_obj(path: str, index_mode: int = OBJ_INDEX_REFERENCE) -> Mesh:
+    """Import an OBJ the way the reference's create_meshes() does (assimp Triangulate|GenNormals,
+    processNode order), through rt_obj_load.  Returns a Mesh (vertex normals, image 0) whose
+    texture_path is the first diffuse texture of its materials."""
+    from . import RtError, lib
+
+    h = c_void_p()
+    rc = lib().rt_obj_load(path.encode(), int(index_mode), ctypes.byref(h))
+    if rc != 0:
+        raise RtError(f"rt_obj_load({path!r}) failed with status {rc}")
+    try:
+        info = ctypes.cast(lib().rt_obj_view(h), POINTER(rt_obj_info)).contents
+        n = info.n_triangles
+        tris = np.ctypeslib.as_array(info.triangles, shape=(n * TRI_FLOATS,)).copy() if n else np.zeros(0, np.float32)
+        m = Mesh(tris, vertex_normals=True, image=0, texture_path=(info.texture or b"").decode())
+        m.n_meshes = info.n_meshes
+        m.n_textures = info.n_textures
+        return m
+    finally:
+        lib().rt_obj_free(h)
+
+
+def mesh_from_arrays(vertices, normals, uvs, faces, index_mode: int = OBJ_INDEX_REFERENCE, image: int = 0) -> Mesh:
+    """create_meshes_d (triangle_mesh.h:147-204) over per-mesh arrays in processNode order, for
+    callers that import meshes themselves: vertices/normals (n_k, 3), uvs (n_k, 2), faces (m_k, 3)
+    per mesh.  OBJ_INDEX_REFERENCE indexes the concatenated arrays with local indices (H16)."""
+    V = np.concatenate([np.asarray(v, np.float32).reshape(-1, 3) for v in vertices])
+    N = np.concatenate([np.asarray(n, np.float32).reshape(-1, 3) for n in normals])
+    UV = np.concatenate([np.asarray(u, np.float32).reshape(-1, 2) for u in uvs])
+    idx, off = [], 0
+    for v, f in zip(vertices, faces):
+        f = np.asarray(f, np.int64).reshape(-1, 3)
+        idx.append(f + (off if index_mode == OBJ_INDEX_GLOBAL else 0))
+        off += len(v)
+    I = np.concatenate(idx)
+    tris = np.concatenate([V[I].reshape(-1, 9), N[I].reshape(-1, 9), UV[I].reshape(-1, 6)], axis=1)
+    return Mesh(tris, vertex_normals=True, image=image)
+
+
+def door_mesh_from_fixture(path: str, index_mode: int = OBJ_INDEX_REFERENCE) -> Mesh:
+    """The C4 door mesh from tests/golden/door_assimp.npz (assimp's import of the reference's
+    assets/door/door.obj, see tests/golden/make_obj_golden.py), for runs where the reference's
+    files are absent (GPU boxes)."""
+    d = np.load(path)
+    n = int(d["n_meshes"][0])
+    return mesh_from_arrays([d[f"v{k}"] for k in range(n)], [d[f"n{k}"] for k in range(n)],
+                            [d[f"uv{k}"] for k in range(n)], [d[f"f{k}"][:, :3] for k in range(n)], index_mode)
