@@ -55,7 +55,8 @@ enum rt_prim_type {
   RT_PRIM_RECT_XY = 2,       /* aarect.h xy_rect  p = x0 x1 y0 y1 k  (x1-x0) (y1-y0)        */
   RT_PRIM_RECT_XZ = 3,       /* aarect.h xz_rect  p = x0 x1 z0 z1 k  (x1-x0) (z1-z0)        */
   RT_PRIM_RECT_YZ = 4,       /* aarect.h yz_rect  p = y0 y1 z0 z1 k  (y1-y0) (z1-z0)        */
-  RT_PRIM_TRIANGLE = 5       /* triangle.h        p[0] = index into rt_scene_soa.triangles  */
+  RT_PRIM_TRIANGLE = 5,      /* triangle.h        p[0] = index into rt_scene_soa.triangles  */
+  RT_PRIM_BOX = 6            /* box.h: the list of six rects  p = x0 y0 z0 x1 y1 z1         */
 };
 /* 48-byte primitive record; three 16-byte loads on the device. */
 typedef struct rt_prim {

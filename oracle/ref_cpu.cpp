@@ -1117,6 +1117,52 @@ static void build_backpack(ref_scene& s) {
   s.cam = Camera(V3(0, 0, -3), V3(0, 0, 0), V3(0, 1, 0), 20, 16.0f / 9.0f, 0.0f, 10.0f, 0, 1);
 }
 
+// Config C5 final scene: the composition defined in rt_scene.cpp (scene_final) / DESIGN.md,
+// restated with the reference's hittable types (box.h boxes under a bvh_node, constant_medium,
+// translate(rotate_y(...)), triangle_mesh).
+static bool build_final(ref_scene& s, const ref_assets* a, Draw& g) {
+  if (!a || a->n_images < 1 || a->n_meshes < 1 || !a->meshes[0].data || a->meshes[0].n_triangles < 3) return false;
+  s.background = kBlack;
+  const Material* ground = s.lam(V3(0.48f, 0.83f, 0.53f));
+  std::vector<const Hittable*> boxes;
+  for (int i = 0; i < 20; ++i)
+    for (int j = 0; j < 20; ++j) {
+      const float w = 100.0f;
+      const float x0 = -1000.0f + (float)i * w, z0 = -1000.0f + (float)j * w, y0 = 0.0f;
+      const float x1 = x0 + w, y1 = g.u(1.0f, 101.0f), z1 = z0 + w;
+      boxes.push_back(s.H<BoxShape>(V3(x0, y0, z0), V3(x1, y1, z1), ground));
+    }
+  List* L = s.H<List>();
+  L->objs.push_back(s.H<RefBvh>(boxes, 0.0f, 1.0f, g));
+  L->objs.push_back(s.H<Rect>(1, 123.0f, 423.0f, 147.0f, 412.0f, 554.0f, s.M<Light>(s.X<Solid>(V3(7, 7, 7)))));
+  const V3 c1(400, 400, 200), c2 = c1 + V3(30, 0, 0);
+  L->objs.push_back(s.H<MovingSphere>(c1, c2, 0.0f, 1.0f, 50.0f, s.lam(V3(0.7f, 0.3f, 0.1f))));
+  L->objs.push_back(s.H<Sphere>(V3(260, 150, 45), 50.0f, s.M<Dielectric>(1.5f)));
+  L->objs.push_back(s.H<Sphere>(V3(0, 150, 145), 50.0f, s.M<Metal>(s.X<Solid>(V3(0.8f, 0.8f, 0.9f)), 1.0f)));
+  const Hittable* boundary = s.H<Sphere>(V3(360, 150, 145), 70.0f, s.M<Dielectric>(1.5f));
+  L->objs.push_back(boundary);
+  L->objs.push_back(s.H<Medium>(boundary, 0.2f, s.M<Isotropic>(s.X<Solid>(V3(0.2f, 0.4f, 0.9f)))));
+  const Hittable* fog = s.H<Sphere>(V3(0, 0, 0), 5000.0f, s.M<Dielectric>(1.5f));
+  L->objs.push_back(s.H<Medium>(fog, 0.0001f, s.M<Isotropic>(s.X<Solid>(V3(1, 1, 1)))));
+  const ref_image& im = a->images[0];
+  L->objs.push_back(s.H<Sphere>(V3(400, 200, 400), 100.0f,
+                                s.M<Lambert>(s.X<ImageTex>(im.data, im.width, im.height, im.bytes_per_pixel))));
+  L->objs.push_back(s.H<Sphere>(V3(220, 280, 300), 80.0f, s.M<Lambert>(s.X<NoiseTex>(g, 0.1f))));
+  const Material* white = s.lam(V3(0.73f, 0.73f, 0.73f));
+  std::vector<const Hittable*> balls;
+  for (int k = 0; k < 1000; ++k) balls.push_back(s.H<Sphere>(g.v3(0.0f, 165.0f), 10.0f, white));
+  L->objs.push_back(s.H<Translate>(s.H<RotateY>(s.H<RefBvh>(balls, 0.0f, 1.0f, g), 15.0f), V3(-100, 270, 395)));
+  ref_mesh m = a->meshes[0];
+  std::vector<float> scaled(m.data, m.data + 24 * (size_t)m.n_triangles);
+  for (int t = 0; t < m.n_triangles; ++t)
+    for (int q = 0; q < 9; ++q) scaled[24 * (size_t)t + q] *= 150.0f;
+  m.data = scaled.data();
+  L->objs.push_back(s.H<Translate>(s.H<RotateY>(build_mesh(s, a, m, g), -30.0f), V3(30, 101, 150)));
+  s.world = L;
+  s.cam = Camera(V3(478, 278, -600), V3(278, 278, 0), V3(0, 1, 0), 40, 16.0f / 9.0f, 0.0f, 10.0f, 0, 1);
+  return true;
+}
+
 // ---------------------------------------------------------------- integrator (render.h:55-113)
 static V3 trace(const ref_scene& s, Ray r, Draw& g, int depth) {
   V3 att(1, 1, 1);
@@ -1190,6 +1236,7 @@ int ref_scene_create_ex(const char* name, int rtl, const ref_assets* a, ref_scen
   else if (n == "earth") { if (!build_earth(*s, a)) return 1; }
   else if (n == "door") { if (!build_mesh_scene(*s, a, g, V3(-3, 4, -5), V3(0, 1, 0))) return 1; }
   else if (n == "cup") { if (!build_mesh_scene(*s, a, g, V3(0, 0, -1), V3(0, 0, 0))) return 1; }
+  else if (n == "final") { if (!build_final(*s, a, g)) return 1; }
   else return 1;
   s->h20 = tl_h20;
   *out = s.release();

@@ -51,6 +51,8 @@ inline Box prim_box(const rt_prim& q, const rt_triangle* tris, float t0, float t
       return Box{{p[0], p[4] - 0.0001f, p[3]}, {p[1], p[4] + 0.0001f, p[3]}};
     case RT_PRIM_RECT_YZ:
       return Box{{p[4] - 0.0001f, p[0], p[2]}, {p[4] + 0.0001f, p[1], p[3]}};
+    case RT_PRIM_BOX:  // box.h:35-38
+      return Box{{p[0], p[1], p[2]}, {p[3], p[4], p[5]}};
     default: {
       const rt_triangle& t = tris[(int)p[0]];
       float v[3][3];

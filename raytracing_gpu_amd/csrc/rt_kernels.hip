@@ -236,16 +236,53 @@ __device__ __forceinline__ void rect_axes(int type, int& ax, int& ia, int& ib) {
   ia = ax == 0 ? 1 : 0;
   ib = ax == 2 ? 1 : 2;
 }
-__device__ __forceinline__ bool rect_t(const Ray& r, const PrimRec& q, int type, float tmin, float tmax, float& t) {
-  int ax, ia, ib;
-  rect_axes(type, ax, ia, ib);
-  const float tt = (q.b.x - comp(r.o, ax)) / comp(r.d, ax);
+// aarect.h hit for the plane comp(ax) = k, a in [a0, a1], b in [b0, b1] over axes (ia, ib).
+__device__ __forceinline__ bool rect_tt(const Ray& r, int ax, int ia, int ib, float a0, float a1, float b0, float b1,
+                                        float k, float tmin, float tmax, float& t) {
+  const float tt = (k - comp(r.o, ax)) / comp(r.d, ax);
   if (tt < tmin || tt > tmax) return false;
   const float a = comp(r.o, ia) + tt * comp(r.d, ia);
   const float b = comp(r.o, ib) + tt * comp(r.d, ib);
-  if (a < q.a.x || a > q.a.y || b < q.a.z || b > q.a.w) return false;
+  if (a < a0 || a > a1 || b < b0 || b > b1) return false;
   t = tt;
   return true;
+}
+__device__ __forceinline__ bool rect_t(const Ray& r, const PrimRec& q, int type, float tmin, float tmax, float& t) {
+  int ax, ia, ib;
+  rect_axes(type, ax, ia, ib);
+  return rect_tt(r, ax, ia, ib, q.a.x, q.a.y, q.a.z, q.a.w, q.b.x, tmin, tmax, t);
+}
+// Face f of box.h's side list (box.h:14-27): xy(z1), xy(z0), xz(y1), xz(y0), yz(x1), yz(x0).
+// lo = (x0 y0 z0), hi = (x1 y1 z1).  Returns the rect type; a0..b1, k its extent and plane.
+__device__ __forceinline__ int box_face(V lo, V hi, int f, float& a0, float& a1, float& b0, float& b1, float& k) {
+  if (f < 2) {
+    a0 = lo.x; a1 = hi.x; b0 = lo.y; b1 = hi.y; k = f == 0 ? hi.z : lo.z;
+    return RT_PRIM_RECT_XY;
+  }
+  if (f < 4) {
+    a0 = lo.x; a1 = hi.x; b0 = lo.z; b1 = hi.z; k = f == 2 ? hi.y : lo.y;
+    return RT_PRIM_RECT_XZ;
+  }
+  a0 = lo.y; a1 = hi.y; b0 = lo.z; b1 = hi.z; k = f == 4 ? hi.x : lo.x;
+  return RT_PRIM_RECT_YZ;
+}
+// box.h hit = hittable_list over the six faces: t_max shrinks, a later face wins ties.
+// Returns the winning face (-1: miss).
+__device__ __forceinline__ int box_t(const Ray& r, const PrimRec& q, float tmin, float tmax, float& t) {
+  const V lo = mk(q.a.x, q.a.y, q.a.z), hi = mk(q.a.w, q.b.x, q.b.y);
+  float closest = tmax;
+  int face = -1;
+  for (int f = 0; f < 6; ++f) {
+    float a0, a1, b0, b1, k, tt;
+    int ax, ia, ib;
+    rect_axes(box_face(lo, hi, f, a0, a1, b0, b1, k), ax, ia, ib);
+    if (rect_tt(r, ax, ia, ib, a0, a1, b0, b1, k, tmin, closest, tt)) {
+      closest = tt;
+      t = tt;
+      face = f;
+    }
+  }
+  return face;
 }
 __device__ __forceinline__ V cross(V a, V b) {
   return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -284,8 +321,13 @@ __device__ __forceinline__ bool prim_t_q(const DScene& S, const PrimRec& q, cons
     if (type == RT_PRIM_MOVING_SPHERE) return sphere_t(r, moving_center(q, r.tm), q.a.w, tmin, tmax, t);
   if constexpr ((F & F_TRI) != 0)
     if (type == RT_PRIM_TRIANGLE) return tri_t(r, S.tris[(int)q.a.x], tmin, tmax, t, bu, bv);
-  if constexpr ((F & F_RECT) != 0)
+  if constexpr ((F & F_RECT) != 0) {
     if (type >= RT_PRIM_RECT_XY && type <= RT_PRIM_RECT_YZ) return rect_t(r, q, type, tmin, tmax, t);
+    if (type == RT_PRIM_BOX) {
+      if constexpr ((F & F_STATS) != 0) nprim += 5;  // six rect hit() calls, as the list counts them
+      return box_t(r, q, tmin, tmax, t) >= 0;
+    }
+  }
   return false;
 }
 template <int F>
@@ -296,7 +338,7 @@ __device__ __forceinline__ bool prim_t(const DScene& S, int pi, const Ray& r, fl
 
 // Full hit record of primitive pi at parameter t (the fields hit() sets on success).
 template <int F>
-__device__ void finalize(const DScene& S, int pi, const Ray& r, float t, Hit& h) {
+__device__ void finalize(const DScene& S, int pi, const Ray& r, float tmin, float t, Hit& h) {
   const PrimRec q = load_prim<F>(S, pi);
   const int tw = __float_as_int(q.c.z);
   const int type = tw & RT_PRIM_TYPE_MASK;
@@ -340,12 +382,21 @@ __device__ void finalize(const DScene& S, int pi, const Ray& r, float t, Hit& h)
    }
   }
   if constexpr ((F & F_RECT) != 0) {  // aarect.h
+    float a0 = q.a.x, b0 = q.a.z, wa = q.b.y, wb = q.b.z;
+    int rt = type;
+    if (type == RT_PRIM_BOX) {  // the face that won: the last one at exactly t in [tmin, t]
+      float tt, a1, b1, k;
+      const int f = box_t(r, q, tmin, t, tt);
+      rt = box_face(mk(q.a.x, q.a.y, q.a.z), mk(q.a.w, q.b.x, q.b.y), f < 0 ? 0 : f, a0, a1, b0, b1, k);
+      wa = a1 - a0;
+      wb = b1 - b0;
+    }
     int ax, ia, ib;
-    rect_axes(type, ax, ia, ib);
+    rect_axes(rt, ax, ia, ib);
     const float a = comp(r.o, ia) + t * comp(r.d, ia);
     const float b = comp(r.o, ib) + t * comp(r.d, ib);
-    h.u = (a - q.a.x) / q.b.y;
-    h.v = (b - q.a.z) / q.b.z;
+    h.u = (a - a0) / wa;
+    h.v = (b - b0) / wb;
     set_face(h, r, mk(ax == 0 ? 1.0f : 0.0f, ax == 1 ? 1.0f : 0.0f, ax == 2 ? 1.0f : 0.0f));
   }
 }
@@ -635,7 +686,7 @@ __device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, fl
       const Ray rr = xform_ray(o, r, moved);
       const rt_object c = S.objects[o.a];
       if (!leaf_closest<F>(S, c, rr, tmin, tmax, t, prim, nnode, nprim, nfall)) return false;
-      finalize<F>(S, prim, rr, t, h);
+      finalize<F>(S, prim, rr, tmin, t, h);
       if (o.b & 2) {
         const float s = o.f[3], cs = o.f[4];
         const V p = mk(cs * h.p.x + s * h.p.z, h.p.y, -s * h.p.x + cs * h.p.z);
@@ -672,7 +723,7 @@ __device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, fl
       return true;
   }
   if (!leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall)) return false;
-  finalize<F>(S, prim, r, t, h);
+  finalize<F>(S, prim, r, tmin, t, h);
   return true;
 }
 
@@ -1159,7 +1210,7 @@ int scene_features(const rt_scene_soa* s) {
   for (int k = 0; k < s->n_prims; ++k) {
     const int t = s->prims[k].type;
     if (t == RT_PRIM_MOVING_SPHERE) f |= F_MOVING;
-    if (t >= RT_PRIM_RECT_XY && t <= RT_PRIM_RECT_YZ) f |= F_RECT;
+    if ((t >= RT_PRIM_RECT_XY && t <= RT_PRIM_RECT_YZ) || t == RT_PRIM_BOX) f |= F_RECT;
     if (t == RT_PRIM_TRIANGLE) f |= F_TRI;
   }
   for (int k = 0; k < s->n_objects; ++k) {

@@ -193,17 +193,9 @@ struct rt_scene_host {
     objects.push_back(o);
     return (int)objects.size() - 1;
   }
-  // box.h:14-27: six rects in a list.
-  int box(F3 p0, F3 p1, int m) {
-    const int first = (int)prims.size();
-    rect(RT_PRIM_RECT_XY, p0.x, p1.x, p0.y, p1.y, p1.z, m);
-    rect(RT_PRIM_RECT_XY, p0.x, p1.x, p0.y, p1.y, p0.z, m);
-    rect(RT_PRIM_RECT_XZ, p0.x, p1.x, p0.z, p1.z, p1.y, m);
-    rect(RT_PRIM_RECT_XZ, p0.x, p1.x, p0.z, p1.z, p0.y, m);
-    rect(RT_PRIM_RECT_YZ, p0.y, p1.y, p0.z, p1.z, p1.x, m);
-    rect(RT_PRIM_RECT_YZ, p0.y, p1.y, p0.z, p1.z, p0.x, m);
-    return object(RT_OBJ_LIST, first, 6);
-  }
+  // box.h:8-40: the list of six rects as one primitive (same hit order and tie rule, box bbox).
+  int box_prim(F3 p0, F3 p1, int m) { return prim(RT_PRIM_BOX, m, {p0.x, p0.y, p0.z, p1.x, p1.y, p1.z}); }
+  int box(F3 p0, F3 p1, int m) { return object(RT_OBJ_PRIM, box_prim(p0, p1, m), 0); }
   // translate(rotate_y(child, deg), off): hittable.h:31-143.
   int xform(int child, float deg, F3 off) {
     const float rad = deg * 3.1415927f / 180.0f;
@@ -516,6 +508,60 @@ void scene_backpack(rt_scene_host& s) {
   s.camera(mk(0, 0, -3), mk(0, 0, 0), mk(0, 1, 0), 20, 16.0f / 9.0f, 0.0f, 10.0f, 0, 1);
 }
 
+// Config C5, final_scene(): the reference has no definition; composed from its components after
+// "Ray Tracing: The Next Week" section 10: 400 ground boxes under a BVH, a light,
+// a moving sphere, glass / metal spheres, a glass sphere filled with a constant medium, a global
+// fog medium, the earth-textured sphere, a perlin sphere, a rotated+translated BVH of 1000
+// spheres and the door mesh (scaled 150x, translated) under its own BVH.  Scene RNG draws, from
+// world_init: 400 box heights (row-major), the ground BVH, the perlin tables, 1000 sphere centres
+// (x, y, z), the sphere BVH, the mesh BVH.
+bool scene_final(rt_scene_host& s, const rt_scene_assets* a) {
+  if (!a || a->n_images < 1 || a->n_meshes < 1 || !a->meshes[0].data || a->meshes[0].n_triangles < 3) return false;
+  set_bg(s, kBlack, 16.0f / 9.0f);
+  SceneRng g;
+  const int ground = s.lam(mk(0.48f, 0.83f, 0.53f));
+  const int gfirst = (int)s.prims.size();
+  for (int i = 0; i < 20; ++i)
+    for (int j = 0; j < 20; ++j) {
+      const float w = 100.0f;
+      const float x0 = -1000.0f + (float)i * w, z0 = -1000.0f + (float)j * w, y0 = 0.0f;
+      const float x1 = x0 + w, y1 = g.u(1.0f, 101.0f), z1 = z0 + w;
+      s.box_prim(mk(x0, y0, z0), mk(x1, y1, z1), ground);
+    }
+  s.world.push_back(s.bvh(gfirst, 400, 0.0f, 1.0f, g));
+  const int light = s.mat(RT_MAT_DIFFUSE_LIGHT, s.solid(mk(7, 7, 7)), 0);
+  s.world.push_back(s.object(RT_OBJ_PRIM, s.rect(RT_PRIM_RECT_XZ, 123, 423, 147, 412, 554, light), 0));
+  const F3 c1 = mk(400, 400, 200), c2 = add(c1, mk(30, 0, 0));
+  s.world.push_back(s.object(RT_OBJ_PRIM, s.moving(c1, c2, 0, 1, 50, s.lam(mk(0.7f, 0.3f, 0.1f))), 0));
+  s.world.push_back(s.object(RT_OBJ_PRIM, s.sphere(mk(260, 150, 45), 50, s.mat(RT_MAT_DIELECTRIC, -1, 1.5f)), 0));
+  s.world.push_back(s.object(RT_OBJ_PRIM,
+                             s.sphere(mk(0, 150, 145), 50, s.mat(RT_MAT_METAL, s.solid(mk(0.8f, 0.8f, 0.9f)), 1.0f)), 0));
+  const int boundary = s.object(RT_OBJ_PRIM, s.sphere(mk(360, 150, 145), 70, s.mat(RT_MAT_DIELECTRIC, -1, 1.5f)), 0);
+  s.world.push_back(boundary);
+  s.world.push_back(s.object(RT_OBJ_MEDIUM, boundary, s.mat(RT_MAT_ISOTROPIC, s.solid(mk(0.2f, 0.4f, 0.9f)), 0),
+                             {-1.0f / 0.2f}));
+  const int fog = s.object(RT_OBJ_PRIM, s.sphere(mk(0, 0, 0), 5000, s.mat(RT_MAT_DIELECTRIC, -1, 1.5f)), 0);
+  s.world.push_back(s.object(RT_OBJ_MEDIUM, fog, s.mat(RT_MAT_ISOTROPIC, s.solid(mk(1, 1, 1)), 0), {-1.0f / 0.0001f}));
+  const int earth = s.mat(RT_MAT_LAMBERTIAN, s.image_tex(a->images[0]), 0.0f);
+  s.world.push_back(s.object(RT_OBJ_PRIM, s.sphere(mk(400, 200, 400), 100, earth), 0));
+  const int pertext = s.noise_tex(RT_TEX_NOISE, g, 0.1f, 0);
+  s.world.push_back(s.object(RT_OBJ_PRIM, s.sphere(mk(220, 280, 300), 80, s.mat(RT_MAT_LAMBERTIAN, pertext, 0)), 0));
+  const int white = s.lam(mk(0.73f, 0.73f, 0.73f));
+  const int sfirst = (int)s.prims.size();
+  for (int k = 0; k < 1000; ++k) s.sphere(g.v3(0.0f, 165.0f), 10, white);
+  s.world.push_back(s.xform(s.bvh(sfirst, 1000, 0.0f, 1.0f, g), 15.0f, mk(-100, 270, 395)));
+  // the door: the mesh with its positions scaled by 150
+  const rt_mesh_asset& m = a->meshes[0];
+  std::vector<float> scaled(m.data, m.data + 24 * (size_t)m.n_triangles);
+  for (int t = 0; t < m.n_triangles; ++t)
+    for (int q = 0; q < 9; ++q) scaled[24 * (size_t)t + q] *= 150.0f;
+  rt_mesh_asset ms = m;
+  ms.data = scaled.data();
+  s.world.push_back(s.xform(add_mesh(s, a, ms, g), -30.0f, mk(30, 101, 150)));
+  s.camera(mk(478, 278, -600), mk(278, 278, 0), mk(0, 1, 0), 40, 16.0f / 9.0f, 0.0f, 10.0f, 0, 1);
+  return true;
+}
+
 int build_named(rt_scene_host& s, const std::string& n, const rt_scene_assets* a) {
   if (n == "basic") scene_basic(s);
   else if (n == "first") scene_first(s);
@@ -530,6 +576,7 @@ int build_named(rt_scene_host& s, const std::string& n, const rt_scene_assets* a
   else if (n == "earth") { if (!scene_earth(s, a)) return RT_ERR_ARG; }
   else if (n == "door") { if (!scene_mesh(s, a, mk(-3, 4, -5), mk(0, 1, 0))) return RT_ERR_ARG; }
   else if (n == "cup") { if (!scene_mesh(s, a, mk(0, 0, -1), mk(0, 0, 0))) return RT_ERR_ARG; }
+  else if (n == "final") { if (!scene_final(s, a)) return RT_ERR_ARG; }
   else return RT_ERR_ARG;
   return RT_OK;
 }

@@ -153,6 +153,32 @@ def test_door_mesh_bit_exact(rtlib, gpu_ctx, oracle, exact):
     assert cnt["segments"] == segs
 
 
+@pytest.mark.parametrize("exact", [False, True], ids=["culled", "exact"])
+def test_final_scene_bit_exact(rtlib, gpu_ctx, oracle, exact):
+    """C5 composition (boxes under a BVH, media, textures, xformed BVHs, the door mesh)."""
+    import os
+
+    import torch
+    from raytracing_gpu_amd import assets
+
+    m = assets.door_mesh_from_fixture(os.path.join(os.path.dirname(__file__), "golden", "door_assimp.npz"))
+    img = assets.synthetic_image(341, 152)
+    W, H, spp, nfb = 80, 45, 2, 2
+    gpu_ctx.upload(rtlib.Scene.builtin("final", images=[img], meshes=[m]))
+    gpu_ctx.render_init(W, H, 1984)
+    fb = torch.zeros(nfb * H * W * 3, dtype=torch.float32, device="cuda")
+    cnt = gpu_ctx.render(rtlib.make_args(W, H, spp, 0, nfb, 50, REF, exact=exact), fb.data_ptr())
+    got = fb.cpu().numpy().reshape(nfb, H, W, 3)
+    ref = oracle.RefScene("final", images=[img], meshes=[(m.tris, True, 0)])
+    segs = 0
+    for f in range(nfb):
+        want, c, _ = ref.render(W, H, spp, f, 50, REF)
+        segs += c["segments"]
+        diff = _bits(got[f]) != _bits(want.reshape(H, W, 3))
+        assert not diff.any(), f"final fb {f}: {int(diff.any(axis=2).sum())} pixels differ"
+    assert cnt["segments"] == segs
+
+
 def test_resolve_matches_average_images(rtlib, gpu_ctx, oracle):
     import torch
 
