@@ -882,12 +882,14 @@ struct RenderParams {
   DScene S;
   const uint4* states;  // 2 uint4 per slot: d v0 v1 v2 | v3 v4 - -
   float* fb;
-  const int32_t* row_map;
+  const int32_t* row_map;     // owned row r -> image row j (output layout order)
+  const int32_t* row_order;   // processing position q -> owned row r (costliest first)
+  unsigned long long* row_cost;  // per image row: segments of the finished items with i % 16 == 0
   unsigned long long* work;
   unsigned long long* counters;  // segments, node, prim, samples
   unsigned long long total_items;
   long long npix;  // W*H of the full image
-  int W, H, rows, spp, fb_first, max_depth, cam_mode, pad;
+  int W, H, rows, spp, fb_first, max_depth, cam_mode, fb_count;
   int pad3, pad4;
   uint32_t cam_state[6];
 #ifdef RT_TRACE
@@ -935,6 +937,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
   Ray ray{};
   V att = mk(1, 1, 1), col = mk(0, 0, 0);
   unsigned long long nseg = 0, nsamp = 0;
+  unsigned item_segs = 0;
   unsigned nnode = 0, nprim = 0, nfall = 0;
   const bool per_pixel = P.cam_mode == RT_CAM_PER_PIXEL;
   const rt_camera& C = S.cam;
@@ -957,11 +960,15 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
           done = true;
         } else {
           item = (long long)mine;
-          const long long per_fb = (long long)P.rows * P.W;
-          f = (int)(item / per_fb);
-          const long long rem = item - (long long)f * per_fb;
-          r = (int)(rem / P.W);
-          i = (int)(rem - (long long)r * P.W);
+          // Row-major, fb inside the row, rows in row_order: the costliest rows of the previous
+          // launch of this configuration first (else bottom to top), so a launch does not end
+          // with a long item started late (a lane runs an item's samples serially).
+          const long long per_row = (long long)P.fb_count * P.W;
+          const int q = (int)(item / per_row);
+          const long long rem = item - (long long)q * per_row;
+          r = P.row_order[q];
+          f = (int)(rem / P.W);
+          i = (int)(rem - (long long)f * P.W);
           j = P.row_map[r];
           const long long id = P.fb_first + f;
           const long long p = (long long)j * P.W + i;
@@ -970,6 +977,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
           loc.d = s0.x; loc.v[0] = s0.y; loc.v[1] = s0.z; loc.v[2] = s0.w; loc.v[3] = s1.x; loc.v[4] = s1.y;
           s = 0;
           depth = 0;
+          item_segs = 0;
           col = mk(0, 0, 0);
         }
       }
@@ -996,6 +1004,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
 
       // ---- one segment (render.h:60-77)
       ++nseg;
+      ++item_segs;
       Hit h;
       bool ended = false;
       V contrib;
@@ -1046,6 +1055,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
           dst[0] = out.x;
           dst[1] = out.y;
           dst[2] = out.z;
+          if (P.row_cost && (i & 15) == 0) atomicAdd(&P.row_cost[j], (unsigned long long)item_segs);  // a sample ranks rows
           item = -1;
         }
       }
@@ -1146,8 +1156,15 @@ struct rt_ctx {
   uint64_t states_seed = 0;
   uint32_t* seq = nullptr;
   unsigned long long* work = nullptr;  // [0] work counter, [1..4] counters
-  int32_t* row_map = nullptr;
+  int32_t* row_map = nullptr;  // [rows] owned row -> image row, then [rows] processing order
   int row_cap = 0;
+  unsigned long long* row_cost = nullptr;  // device, per image row
+  int row_cost_cap = 0;
+  // Per-row cost of the last launch of (scene generation, W, H, spp, depth): the schedule of the
+  // next launch of that configuration (no pixel result depends on the order).
+  std::vector<unsigned long long> host_cost;
+  long long cost_key[5] = {-1, -1, -1, -1, -1};
+  long long scene_gen = 0;
   int cus = 0, blocks_per_cu[16] = {0};
   int features = 0;
   int dev_nodes = 0, dev_prims = 0;  // device array sizes (for LDS staging)
@@ -1464,6 +1481,7 @@ int rt_ctx_destroy(rt_ctx* c) {
   if (c->seq) (void)hipFree(c->seq);
   if (c->work) (void)hipFree(c->work);
   if (c->row_map) (void)hipFree(c->row_map);
+  if (c->row_cost) (void)hipFree(c->row_cost);
   if (c->dbg) (void)hipFree(c->dbg);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1486,6 +1504,7 @@ int32_t rt_owned_rows(const rt_render_args* a, int32_t* rows) {
 }
 
 int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
+  if (c) ++c->scene_gen;  // invalidates the row-cost schedule
   if (!c || !s) return RT_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   if (s->n_world <= 0 || !s->world || s->n_objects <= 0 || s->n_materials <= 0)
@@ -1595,19 +1614,37 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   if (rows > c->row_cap) {
     if (c->row_map) HIPCHK(c, hipFree(c->row_map));
     c->row_map = nullptr;
-    HIPCHK(c, hipMalloc((void**)&c->row_map, rows * sizeof(int32_t)));
+    HIPCHK(c, hipMalloc((void**)&c->row_map, 2 * (size_t)rows * sizeof(int32_t)));
     c->row_cap = rows;
   }
-  std::vector<int32_t> rm(rows);
+  if (a->height > c->row_cost_cap) {
+    if (c->row_cost) HIPCHK(c, hipFree(c->row_cost));
+    c->row_cost = nullptr;
+    HIPCHK(c, hipMalloc((void**)&c->row_cost, (size_t)a->height * sizeof(unsigned long long)));
+    c->row_cost_cap = a->height;
+  }
+  std::vector<int32_t> rm(2 * (size_t)rows);
   rt_owned_rows(a, rm.data());
-  HIPCHK(c, hipMemcpyAsync(c->row_map, rm.data(), rows * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  const long long key[5] = {c->scene_gen, a->width, a->height, a->spp, a->max_depth};
+  const bool have_cost = std::equal(key, key + 5, c->cost_key) && (int)c->host_cost.size() == a->height;
+  for (int q = 0; q < rows; ++q) rm[rows + q] = q;
+  // Costliest rows first only when lanes get few items each (a rank's share of a multi-GPU
+  // image): there the launch ends with its last long item; with many items per lane bottom-to-top
+  // order (sky last in the reference's scenes) measures faster.
+  const long long items = (long long)a->fb_count * rows * a->width;
+  if (have_cost && items < 8LL * c->cus * 1024)
+    std::stable_sort(rm.begin() + rows, rm.end(), [&](int x, int y) { return c->host_cost[rm[x]] > c->host_cost[rm[y]]; });
+  HIPCHK(c, hipMemcpyAsync(c->row_map, rm.data(), 2 * (size_t)rows * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->work, 0, 8 * sizeof(unsigned long long), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->row_cost, 0, (size_t)a->height * sizeof(unsigned long long), c->stream));
 
   RenderParams P{};
   P.S = c->scene;
   P.states = c->states;
   P.fb = fb_dev;
   P.row_map = c->row_map;
+  P.row_order = c->row_map + rows;
+  P.row_cost = have_cost ? nullptr : c->row_cost;  // measured once per configuration
   P.work = c->work;
   P.counters = c->work + 1;
   P.total_items = (unsigned long long)a->fb_count * rows * a->width;
@@ -1617,6 +1654,7 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   P.rows = rows;
   P.spp = a->spp;
   P.fb_first = a->fb_first;
+  P.fb_count = a->fb_count;
   P.max_depth = a->max_depth;
   P.cam_mode = a->cam_mode;
   const rtx::State cs = rtx::seed_state(a->seed);  // pristine slot 0 = curand_init(seed, 0, 0)
@@ -1645,8 +1683,15 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   P.S.lds_prims = lds_var ? c->dev_prims : 0;
   const size_t shmem = (lds_var ? lds_bytes : 0) + (size_t)bs * kStackDepth * 4;
   const long long resident = (long long)c->cus * std::max(1, c->blocks_per_cu[var]);
-  const long long need = (long long)((P.total_items + bs - 1) / bs);
-  const unsigned blocks = (unsigned)std::max(1LL, std::min(resident, need));
+  // Persistent grid: every resident workgroup, even when there are fewer items than lanes (a
+  // rank of a multi-GPU run): waves take items dynamically, so the items spread over all CUs
+  // instead of packing into the first ceil(items / block) of them.
+#ifdef RT_GRID_PACKED
+  const long long cap = (long long)((P.total_items + bs - 1) / bs);
+#else
+  const long long cap = resident;
+#endif
+  const unsigned blocks = (unsigned)std::max(1LL, std::min(resident, cap));
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
 #ifdef RT_STAMPS
   static unsigned long long* sbuf = nullptr;
@@ -1667,7 +1712,16 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   unsigned long long host_cnt[8];
   HIPCHK(c, hipMemcpyAsync(host_cnt, c->work, sizeof(host_cnt), hipMemcpyDeviceToHost, c->stream));
+  std::vector<unsigned long long> cost((size_t)a->height);
+  HIPCHK(c, hipMemcpyAsync(cost.data(), c->row_cost, cost.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (!have_cost) {
+    c->host_cost.assign((size_t)a->height, 0ull);
+    std::copy(key, key + 5, c->cost_key);
+  }
+  if (!have_cost)
+    for (int q = 0; q < rows; ++q) c->host_cost[rm[q]] = cost[rm[q]];
   HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
   if (counters) {
     counters->segments = host_cnt[1];
