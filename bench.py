@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--nfb", type=int, default=10, help="no_fb")
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--cam", choices=["ref", "per_pixel"], default="ref")
-    ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--band-rows", type=int, default=4, help="rows per band (800 rows = 200 bands: equal shares at N = 1, 2, 4, 8)")
     ap.add_argument("--exact", action="store_true", help="reference BVH visit set (no culling)")
     ap.add_argument("--no-lds", action="store_true", help="keep the scene in global memory")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
