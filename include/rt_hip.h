@@ -286,6 +286,14 @@ typedef struct rt_obj_info {
   const char* texture;   /* first diffuse texture path (OBJ directory + map_Kd), "" if none     */
 } rt_obj_info;
 int rt_obj_load(const char* path, int32_t index_mode, rt_obj_mesh** out);
+/* Image decoding for textures: make_image()/imread() (texture.h:166-203) through the reference's
+ * stb_image v2.26, restated for baseline JPEGs (csrc/rt_image.cpp): identical texel bytes.
+ * Output = stbi_load(.., 0) layout (rows top to bottom, 1 or 3 channels). */
+typedef struct rt_image_host rt_image_host;
+int rt_image_decode(const uint8_t* bytes, int64_t n, rt_image_host** out);
+int rt_image_load(const char* path, rt_image_host** out);
+const rt_image_asset* rt_image_view(const rt_image_host* im);
+void rt_image_free(rt_image_host* im);
 const rt_obj_info* rt_obj_view(const rt_obj_mesh* m);
 void rt_obj_free(rt_obj_mesh* m);
 

@@ -115,6 +115,10 @@ ABI = {
     "rt_obj_load": (c_int, [c_char_p, c_int, POINTER(c_void_p)]),
     "rt_obj_view": (c_void_p, [c_void_p]),
     "rt_obj_free": (None, [c_void_p]),
+    "rt_image_decode": (c_int, [c_void_p, ctypes.c_int64, POINTER(c_void_p)]),
+    "rt_image_load": (c_int, [c_char_p, POINTER(c_void_p)]),
+    "rt_image_view": (c_void_p, [c_void_p]),
+    "rt_image_free": (None, [c_void_p]),
     "rt_scene_view": (POINTER(rt_scene_soa), [c_void_p]),
     "rt_scene_free": (None, [c_void_p]),
 }

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librt_hip.so")
 
-HIP_SOURCES = ["rt_kernels.hip", "rt_scene.cpp", "rt_obj.cpp"]
+HIP_SOURCES = ["rt_kernels.hip", "rt_scene.cpp", "rt_obj.cpp", "rt_image.cpp"]
 HIP_DEPS = HIP_SOURCES + ["rt_detmath.h", "rt_xorwow.h", "rt_host_geom.h"]
 # -ffp-contract=off: no FMA contraction anywhere, so every float op rounds like the reference's
 # C++ source and like the CPU oracle; fp32 div/sqrt correctly rounded (IEEE) on the device.
@@ -50,6 +50,9 @@ def build_oracle(force: bool = False) -> str:
     if force:
         subprocess.run(["make", "-C", odir, "clean"], check=True)
     subprocess.run(args, check=True, stdout=subprocess.DEVNULL)
+    # the reference's own vendored stb_image, compiled where it lies (test pin for image decoding)
+    if os.path.exists("/root/reference/external/stb_image.h"):
+        subprocess.run(["make", "-C", odir, "ref"], check=True, stdout=subprocess.DEVNULL)
     return os.path.join(odir, "_build", "libref_cpu.so")
 
 

@@ -4,9 +4,8 @@ The reference reads these files while it builds a scene: stbi_load for textures
 (texture.h:166-203, make_image) and assimp for OBJ meshes (triangle_mesh.h:129-352,
 create_meshes).  Here the host decodes them and passes plain arrays through the C ABI:
 
-- `load_image(path)` decodes with Pillow (libjpeg).  The reference uses stb_image v2.26; the two
-  decoders may differ in the last bit of some texels, so texel bytes are "parity unpinned" against
-  the reference's loader (the render of given texels is bit-exact between GPU and oracle).
+- `load_image(path)` decodes JPEGs with the native decoder restating stb_image v2.26 (the
+  reference's vendored loader) bit-exactly, and lossless formats with Pillow.
 - `synthetic_image(w, h)` is a deterministic texture of any shape (tests and benchmarks on a GPU
   box, where the reference's files do not exist).
 """
@@ -48,8 +47,31 @@ class Mesh:
         return self.tris.shape[0]
 
 
+def decode_jpeg(data: bytes) -> np.ndarray:
+    """Baseline JPEG -> HxWxC uint8 with stb_image v2.26's arithmetic (rt_image_decode): the texel
+    bytes the reference's make_image() uploads."""
+    from . import RtError, lib
+
+    h = c_void_p()
+    buf = np.frombuffer(data, np.uint8)
+    rc = lib().rt_image_decode(buf.ctypes.data, len(buf), ctypes.byref(h))
+    if rc != 0:
+        raise RtError(f"rt_image_decode failed with status {rc} (not a baseline grey/YCbCr JPEG?)")
+    try:
+        v = ctypes.cast(lib().rt_image_view(h), POINTER(rt_image_asset)).contents
+        n = v.width * v.height * v.bytes_per_pixel
+        return np.ctypeslib.as_array(v.data, shape=(n,)).copy().reshape(v.height, v.width, v.bytes_per_pixel)
+    finally:
+        lib().rt_image_free(h)
+
+
 def load_image(path: str) -> np.ndarray:
-    """Decode an image file to HxWxC uint8 (the channel count of the file, like stbi_load(.., 0))."""
+    """Decode an image file to HxWxC uint8 like stbi_load(path, .., 0).  JPEGs go through the native
+    stb-exact decoder; lossless formats (PNG, ...) through Pillow, whose bytes are the file's."""
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[:2] == b"\xff\xd8":
+        return decode_jpeg(data)
     from PIL import Image
 
     im = Image.open(path)
