@@ -60,6 +60,7 @@ enum : int {
   F_ALL = (1 << 11) - 2,
   F_SPHERES = F_MOVING | F_CHECKER | F_BVH,           // basic, first, big1 (C2), two_spheres
   F_CORNELL = F_RECT | F_LIST | F_XFORM | F_MEDIUM,   // cornell, cornell_smoke (C3)
+  F_MESH = F_TRI | F_IMAGE | F_BVH | F_LIST,            // triangle meshes with image textures (C4)
 };
 
 namespace {
@@ -287,40 +288,39 @@ __device__ __forceinline__ int box_t(const Ray& r, const PrimRec& q, float tmin,
 __device__ __forceinline__ V cross(V a, V b) {
   return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
-// Moller-Trumbore, triangle.h:120-147 (bitwise | of the reference kept as a non-short-circuit or).
-__device__ __forceinline__ bool tri_t(const Ray& r, const rt_triangle& T, float tmin, float tmax, float& t, float& bu,
-                                      float& bv) {
+// Moller-Trumbore, triangle.h:120-147 (bitwise | of the reference kept as a non-short-circuit or),
+// on the operands the device record carries: v0 = p[0..2], e0 = p[3..5], e1 = p[6..8].
+__device__ __forceinline__ bool tri_t(const Ray& r, const PrimRec& q, float tmin, float tmax, float& t) {
   const float eps = 0.0000001f;
-  const V e0 = ld3(T.e0), e1 = ld3(T.e1);
+  const V v0 = mk(q.a.x, q.a.y, q.a.z), e0 = mk(q.a.w, q.b.x, q.b.y), e1 = mk(q.b.z, q.b.w, q.c.x);
   const V h = cross(r.d, e1);
   const float a = dot(e0, h);
   if (a > -eps && a < eps) return false;
   const float f = 1.0f / a;
-  const V s = r.o - ld3(T.v0);
+  const V s = r.o - v0;
   const float u = f * dot(s, h);
   if (u < 0.0f || u > 1.0f) return false;
-  const V q = cross(s, e0);
-  const float v = f * dot(r.d, q);
+  const V qq = cross(s, e0);
+  const float v = f * dot(r.d, qq);
   if ((v < 0.0f) | (u + v > 1.0f)) return false;
-  const float tt = f * dot(e1, q);
+  const float tt = f * dot(e1, qq);
   if (tt < tmin || tt > tmax || tt < eps) return false;
   t = tt;
-  bu = u;
-  bv = v;
   return true;
 }
+// Index of a triangle primitive's 144-byte record (type word bits 12..31, set at upload).
+__device__ __forceinline__ int tri_index(const PrimRec& q) { return __float_as_int(q.c.z) >> 12; }
 
 template <int F>
 __device__ __forceinline__ bool prim_t_q(const DScene& S, const PrimRec& q, const Ray& r, float tmin, float tmax,
                                          float& t, unsigned& nprim) {
   if constexpr ((F & F_STATS) != 0) ++nprim;
   const int type = prim_type(q);
-  float bu, bv;
   if (type == RT_PRIM_SPHERE) return sphere_t(r, mk(q.a.x, q.a.y, q.a.z), q.a.w, tmin, tmax, t);
   if constexpr ((F & F_MOVING) != 0)
     if (type == RT_PRIM_MOVING_SPHERE) return sphere_t(r, moving_center(q, r.tm), q.a.w, tmin, tmax, t);
   if constexpr ((F & F_TRI) != 0)
-    if (type == RT_PRIM_TRIANGLE) return tri_t(r, S.tris[(int)q.a.x], tmin, tmax, t, bu, bv);
+    if (type == RT_PRIM_TRIANGLE) return tri_t(r, q, tmin, tmax, t);
   if constexpr ((F & F_RECT) != 0) {
     if (type >= RT_PRIM_RECT_XY && type <= RT_PRIM_RECT_YZ) return rect_t(r, q, type, tmin, tmax, t);
     if (type == RT_PRIM_BOX) {
@@ -362,7 +362,7 @@ __device__ void finalize(const DScene& S, int pi, const Ray& r, float tmin, floa
   }
   if constexpr ((F & F_TRI) != 0) {
    if (type == RT_PRIM_TRIANGLE) {  // triangle.h:151-175
-    const rt_triangle& T = S.tris[(int)q.a.x];
+    const rt_triangle& T = S.tris[tri_index(q)];
     const V v2 = h.p - ld3(T.v0);
     const V e0 = ld3(T.e0), e1 = ld3(T.e1);
     const float d20 = dot(v2, e0), d21 = dot(v2, e1);
@@ -1195,9 +1195,12 @@ const Variant kVariants[] = {
     RT_VARIANT(F_CORNELL),
     RT_VARIANT(F_CORNELL | F_EXACT),
     RT_VARIANT(F_CORNELL | F_EXACT | F_STATS),
+    RT_VARIANT(F_MESH),
+    RT_VARIANT(F_MESH | F_STATS),
+    RT_VARIANT(F_MESH | F_EXACT),
 };
 #undef RT_VARIANT
-constexpr int kNumVariants = 15;
+constexpr int kNumVariants = 18;
 constexpr int kLdsBudget = 156 * 1024;  // bytes of staged nodes + primitives + stacks per workgroup
 
 // Smallest compiled variant that covers the scene's features and the requested mode.
@@ -1544,6 +1547,21 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
       if (fast < 0) return fail(c, RT_ERR_SCENE, "malformed reference bvh");
       o.c = fast;
     }
+  }
+  // Triangles: the Moller-Trumbore operands (v0, e0, e1) in p[0..8] of the device record and the
+  // triangle's index in the type word's bits 12..31, so a hit test is one 48-byte fetch; the
+  // 144-byte record is read only for the winner's hit record.
+  for (rt_prim& p : prims) {
+    if ((p.type & 0xff) != RT_PRIM_TRIANGLE) continue;
+    const int ti = (int)p.p[0];
+    if (ti < 0 || ti >= s->n_triangles || ti >= (1 << 19)) return fail(c, RT_ERR_SCENE, "triangle index out of range");
+    const rt_triangle& t = s->triangles[ti];
+    for (int k = 0; k < 3; ++k) {
+      p.p[k] = t.v0[k];
+      p.p[3 + k] = t.e0[k];
+      p.p[6 + k] = t.e1[k];
+    }
+    p.type |= ti << 12;
   }
   DScene& d = c->scene;
   d = DScene{};
