@@ -222,6 +222,73 @@ static void trace_inline(const Tree& T, const Ray& r, Stats& st) {
   }
 }
 
+
+// 4-wide collapse of a binary tree: each node takes its children, replacing inner children by
+// their two children (2..4 children per node); leaves stay leaves (one primitive each).
+struct Node4 {
+  Box cb[4];
+  int child[4];  // >= 0: Node4 index, < 0: leaf
+  int n = 0;
+};
+static int collapse4(const Tree& T, int k, std::vector<Node4>& out) {
+  const int me = (int)out.size();
+  out.push_back(Node4{});
+  Node4 m;
+  const Node& b = T.nodes[k];
+  std::vector<std::pair<Box, int>> kids;
+  for (int c = 0; c < 2; ++c) {
+    if (b.child[c] < 0) {
+      kids.push_back({b.cb[c], b.child[c]});
+    } else {
+      const Node& g = T.nodes[b.child[c]];
+      for (int d = 0; d < 2; ++d) kids.push_back({g.cb[d], g.child[d]});
+    }
+  }
+  for (auto& kd : kids) {
+    m.cb[m.n] = kd.first;
+    m.child[m.n] = kd.second;  // binary index for now
+    ++m.n;
+  }
+  for (int c = 0; c < m.n; ++c)
+    if (m.child[c] >= 0) m.child[c] = collapse4(T, m.child[c], out);
+  out[me] = m;
+  return me;
+}
+static void trace4(const Tree& T, const std::vector<Node4>& N, const Ray& r, Stats& st) {
+  float best = INFINITY;
+  int stack[128], sp = 0;
+  int cur = 0;
+  for (;;) {
+    st.steps++;
+    const Node4& n = N[cur];
+    const float cut = best * 1.0039f;
+    float tt[4];
+    int hit_inner[4], ni = 0;
+    for (int c = 0; c < n.n; ++c) {
+      st.box += 1;
+      if (!box_hit(n.cb[c], r, cut, tt[c])) continue;
+      if (n.child[c] < 0) {
+        float t;
+        st.prim++;
+        for (int id : T.leaves[-n.child[c] - 1])
+          if (prim_hit(id, r, t) && t < best) best = t;
+      } else {
+        hit_inner[ni++] = c;
+      }
+    }
+    // nearest first: push the others far-to-near
+    std::sort(hit_inner, hit_inner + ni, [&](int a, int b) { return tt[a] > tt[b]; });
+    for (int q = 0; q + 1 < ni; ++q) stack[sp++] = n.child[hit_inner[q]];
+    st.maxstack = std::max(st.maxstack, (double)sp);
+    if (ni > 0) {
+      cur = n.child[hit_inner[ni - 1]];
+      continue;
+    }
+    if (sp == 0) break;
+    cur = stack[--sp];
+  }
+}
+
 int main(int argc, char** argv) {
   const char* rays_path = argc > 1 ? argv[1] : "/tmp/c2_rays.bin";
   FILE* f = fopen(rays_path, "rb");
@@ -298,6 +365,20 @@ int main(int argc, char** argv) {
       printf("steps p50 %d p90 %d p99 %d; mean over consecutive 64-ray groups of max steps: %.1f\n", p50, p90, p99, wave_max / wave_sum);
       printf("%-18s nodes %4zu depth %2d | per ray: box %6.2f prim %5.2f steps %5.2f maxstack %2.0f\n",
              "sah1-inline-prims", T.nodes.size(), md, st.box / nr, st.prim / nr, st.steps / nr, st.maxstack);
+      std::vector<Node4> N4;
+      collapse4(T, 0, N4);
+      Stats s4;
+      double wmax = 0, wsum = 0;
+      int ln = 0, cm = 0;
+      for (const Ray& r : rays) {
+        Stats one;
+        trace4(T, N4, r, one);
+        s4.box += one.box; s4.prim += one.prim; s4.steps += one.steps; s4.maxstack = std::max(s4.maxstack, one.maxstack);
+        cm = std::max(cm, (int)one.steps);
+        if (++ln == 64) { wmax += cm; wsum += 1; ln = 0; cm = 0; }
+      }
+      printf("%-18s nodes %4zu        | per ray: box %6.2f prim %5.2f steps %5.2f maxstack %2.0f wave-max steps %.1f\n",
+             "sah1-bvh4", N4.size(), s4.box / nr, s4.prim / nr, s4.steps / nr, s4.maxstack, wmax / wsum);
     }
   }
   printf("rays %zu\n", nr);
