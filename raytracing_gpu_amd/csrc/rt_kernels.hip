@@ -108,9 +108,16 @@ template <int F>
 constexpr int render_block() {
   return (F & F_LDS) != 0 ? 1024 : 256;
 }
+// Validation margins (F_LDS: staged after the primitives, two per float4).
+template <int F>
+__device__ __forceinline__ const float2* pmargin_of(const DScene& S) {
+  if constexpr ((F & F_LDS) != 0) return (const float2*)(rt_lds + 2 * S.lds_nodes + 3 * S.lds_prims);
+  else return S.pmargin;
+}
 template <int F>
 __device__ __forceinline__ int* stack_of(const DScene& S) {
-  if constexpr ((F & F_LDS) != 0) return (int*)(rt_lds + 2 * S.lds_nodes + 3 * S.lds_prims) + threadIdx.x;
+  if constexpr ((F & F_LDS) != 0)
+    return (int*)(rt_lds + 2 * S.lds_nodes + 3 * S.lds_prims + (S.lds_prims + 1) / 2) + threadIdx.x;
   else return (int*)rt_lds + threadIdx.x;
 }
 
@@ -602,7 +609,7 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
     // spheres, slab rounding 2^-22 of the distance) cannot reject this ray, so only the other
     // chain positions are tested.  pmargin = {bitmask of chain positions with margin < 0.05,
     // smallest margin among the rest} (computed at upload).
-    const float2 pm = S.pmargin[best_prim];
+    const float2 pm = pmargin_of<F>(S)[best_prim];
     const float dmax = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)),
                                        __builtin_fabsf(r.d.z));
     const float bound = 0.001953125f * best * dmax;  // 2^-9 * t * |d|_inf
@@ -919,9 +926,11 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
   const DScene& S = P.S;
   if constexpr ((F & F_LDS) != 0) {
     // Stage nodes and primitives (read-only, scene-sized) in LDS once per workgroup.
-    const int nn = 2 * P.S.lds_nodes, np = 3 * P.S.lds_prims;
+    const int nn = 2 * P.S.lds_nodes, np = 3 * P.S.lds_prims, nm = (P.S.lds_prims + 1) / 2;
     for (int q = threadIdx.x; q < nn; q += render_block<F>()) rt_lds[q] = P.S.nodes[q];
     for (int q = threadIdx.x; q < np; q += render_block<F>()) rt_lds[nn + q] = P.S.prims[q];
+    const float4* pm = (const float4*)P.S.pmargin;  // padded to an even count at upload
+    for (int q = threadIdx.x; q < nm; q += render_block<F>()) rt_lds[nn + np + q] = pm[q];
     __syncthreads();
   }
   const unsigned lane = __lane_id();
@@ -1575,6 +1584,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   if ((rc = upload(c, s->triangles, (size_t)s->n_triangles, &d.tris))) return rc;
   if ((rc = upload(c, nodes.data(), nodes.size(), &dn))) return rc;
   if ((rc = upload(c, s->materials, (size_t)s->n_materials, &dm))) return rc;
+  if (pmargin.size() & 1) pmargin.push_back(make_float2(-INFINITY, -INFINITY));  // whole float4s for LDS staging
   if ((rc = upload(c, pmargin.data(), pmargin.size(), &d.pmargin))) return rc;
   if ((rc = upload(c, s->textures, (size_t)s->n_textures, &d.texs))) return rc;
   if ((rc = upload(c, s->perlins, (size_t)s->n_perlins, &d.perlins))) return rc;
@@ -1681,7 +1691,7 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
 
   const bool stats = a->stats != 0;
   const bool check = (a->flags & RT_FLAG_AUDIT) != 0;
-  const size_t lds_bytes = (size_t)(2 * c->dev_nodes + 3 * c->dev_prims) * sizeof(float4);
+  const size_t lds_bytes = (size_t)(2 * c->dev_nodes + 3 * c->dev_prims + (c->dev_prims + 1) / 2) * sizeof(float4);
   const bool use_lds = lds_bytes + 1024 * kStackDepth * 4 <= (size_t)kLdsBudget && (a->flags & RT_FLAG_NO_LDS) == 0;
   const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
                                (a->flags & RT_FLAG_WIDEST) != 0);
