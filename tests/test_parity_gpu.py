@@ -297,3 +297,50 @@ def test_render_init_states_match_curand_init(rtlib, gpu_ctx, oracle):
     gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "xorwow_uniforms.json")))
     for s, words in gold["states"].items():
         assert np.array_equal(gpu_ctx.read_states(int(s), 1)[0], np.array(words, np.uint32))
+
+
+EDGE = [
+    # scene, W, H, spp, fb_first, fb_count, cam, depth
+    ("basic", 1, 1, 3, 0, 2, REF, 50),          # N = 1: every slot is 0
+    ("basic", 200, 100, 1, 0, 1, REF, 1),       # config C1: depth 1, explicit height
+    ("big1", 7, 3, 5, 37, 2, REF, 50),          # odd sizes, a large fb id
+    ("cornell_smoke", 17, 13, 3, 0, 3, PIX, 2),  # per-pixel camera, depth 2 through the media
+    ("two_perlin", 33, 9, 1, 5, 1, REF, 3),
+]
+
+
+@pytest.mark.parametrize("scene,W,H,spp,fb_first,fb_count,cam,depth", EDGE)
+def test_edge_configs_bit_exact(rtlib, gpu_ctx, oracle, scene, W, H, spp, fb_first, fb_count, cam, depth):
+    gpu, rows, cnt, _, _ = _gpu_render(rtlib, gpu_ctx, scene, W, H, spp, fb_first, fb_count, cam, depth=depth)
+    ref = oracle.RefScene(scene)
+    segs = 0
+    for f in range(fb_count):
+        fb, c, _ = ref.render(W, H, spp, fb_first + f, depth, cam)
+        segs += c["segments"]
+        assert np.array_equal(_bits(gpu[f]), _bits(fb.reshape(H, W, 3))), f"{scene} fb {fb_first + f}"
+    assert cnt["segments"] == segs
+
+
+def test_abi_error_contract(rtlib):
+    """Every call reports failure through its status and rt_last_error; nothing aborts."""
+    import torch
+
+    ctx = rtlib.Context(0)
+    fb = torch.zeros(64 * 36 * 3, dtype=torch.float32, device="cuda")
+    args = rtlib.make_args(64, 36, 1)
+    with pytest.raises(rtlib.RtError, match="no scene"):
+        ctx.render(args, fb.data_ptr())
+    ctx.upload(rtlib.Scene.builtin("basic"))
+    with pytest.raises(rtlib.RtError, match="render_init"):
+        ctx.render(args, fb.data_ptr())
+    ctx.render_init(64, 36, 1984)
+    with pytest.raises(rtlib.RtError, match="render_init"):
+        ctx.render(rtlib.make_args(65, 36, 1), fb.data_ptr())
+    with pytest.raises(rtlib.RtError):
+        ctx.render(args, 0)
+    with pytest.raises(rtlib.RtError, match="band"):
+        ctx.render(rtlib.make_args(64, 36, 1, band_rows=8, band_first=3, band_stride=2), fb.data_ptr())
+    with pytest.raises(rtlib.RtError):
+        ctx.render(rtlib.make_args(64, 36, 0), fb.data_ptr())
+    ctx.render(args, fb.data_ptr())  # still usable after the failures
+    ctx.close()
