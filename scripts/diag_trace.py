@@ -11,12 +11,13 @@ from oracle import ref_cpu
 
 scene = sys.argv[1]; W, H, spp, nfb = [int(x) for x in sys.argv[2:6]]
 fl = set(sys.argv[6:])
+FB = int(next((x[3:] for x in fl if x.startswith("fb=")), "0"))  # fb id to compare
 kw = dict(exact="exact" in fl, widest="widest" in fl, lds="nolds" not in fl, stats="stats" in fl)
 ctx = rt.Context(0); ctx.upload(rt.Scene.builtin(scene)); ctx.render_init(W, H, 1984)
 ref = ref_cpu.RefScene(scene)
-want = ref.render(W, H, spp, 0, 50, 0)[0].reshape(H, W, 3)
+want = ref.render(W, H, spp, FB, 50, 0)[0].reshape(H, W, 3)
 fb = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
-ctx.render(rt.make_args(W, H, spp, 0, 1, 50, 0, **kw), fb.data_ptr())
+ctx.render(rt.make_args(W, H, spp, FB, 1, 50, 0, **kw), fb.data_ptr())
 got = fb.cpu().numpy().reshape(H, W, 3)
 d = np.argwhere((got.view(np.uint32) != want.view(np.uint32)).any(axis=2))
 print("diff pixels", len(d))
@@ -26,7 +27,7 @@ j, i = [int(x) for x in d[0]]
 print("pixel", i, j, "gpu", got[j, i], "ref", want[j, i])
 os.environ["RT_TRACE_ITEM"] = str(j * W + i)
 os.environ["RT_TRACE_OUT"] = "/tmp/trace.bin"
-ctx.render(rt.make_args(W, H, spp, 0, 1, 50, 0, **kw), fb.data_ptr())
+ctx.render(rt.make_args(W, H, spp, FB, 1, 50, 0, **kw), fb.data_ptr())
 t = np.fromfile("/tmp/trace.bin", np.float32).reshape(256, 16)
 n = int(t[0].view(np.uint32)[0])
 g = t[1:1 + min(n, 255)]
@@ -37,7 +38,7 @@ RL.ref_capture_rays.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
 cap = np.zeros((100000, 8), np.float32)
 RL.ref_capture_rays(cap.ctypes.data, len(cap))
 segs = np.zeros(W * H, np.int32)
-_, _, sp = ref.render(W, H, spp, 0, 50, 0, rows=(j, H), threads=1, seg_per_pixel=True)
+_, _, sp = ref.render(W, H, spp, FB, 50, 0, rows=(j, H), threads=1, seg_per_pixel=True)
 ncap = RL.ref_capture_rays(None, 0)
 before = int(sp[j * W:j * W + i].sum())
 r = cap[before:before + int(sp[j * W + i])]
