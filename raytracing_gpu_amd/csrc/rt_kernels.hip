@@ -609,10 +609,29 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
     // spheres, slab rounding 2^-22 of the distance) cannot reject this ray, so only the other
     // chain positions are tested.  pmargin = {bitmask of chain positions with margin < 0.05,
     // smallest margin among the rest} (computed at upload).
-    const float2 pm = pmargin_of<F>(S)[best_prim];
     const float dmax = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)),
                                        __builtin_fabsf(r.d.z));
     const float bound = 0.001953125f * best * dmax;  // 2^-9 * t * |d|_inf
+    {
+      // Every reference ancestor contains the winner's box, so a computed hit point deeper inside
+      // the winner's own box than `bound` passes all of them: a sphere touches its box only at
+      // six points, so the chain is rarely tested at all.  (Moving spheres: the box at the ray's
+      // time lies inside the box over the shutter.  A negative radius inverts the box: no skip.)
+      const PrimRec q = load_prim<F>(S, best_prim);
+      const int ty = prim_type(q);
+      if (ty == RT_PRIM_SPHERE || ((F & F_MOVING) != 0 && ty == RT_PRIM_MOVING_SPHERE)) {
+        V c = mk(q.a.x, q.a.y, q.a.z);
+        if constexpr ((F & F_MOVING) != 0)
+          if (ty == RT_PRIM_MOVING_SPHERE) c = moving_center(q, r.tm);
+        const V p = r.o + best * r.d;
+        const float rad = q.a.w;
+        const float mx = __builtin_fminf(p.x - (c.x - rad), (c.x + rad) - p.x);
+        const float my = __builtin_fminf(p.y - (c.y - rad), (c.y + rad) - p.y);
+        const float mz = __builtin_fminf(p.z - (c.z - rad), (c.z + rad) - p.z);
+        if (__builtin_fminf(__builtin_fminf(mx, my), mz) > bound) return true;
+      }
+    }
+    const float2 pm = pmargin_of<F>(S)[best_prim];
     const unsigned must = bound < pm.y ? __float_as_uint(pm.x) : 0xffffffffu;
     int pos = 0;
     for (int kr = last0 + (best_rank >> 1);; kr = (kr - 1) >> 1, ++pos) {
