@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the untimed node/prim counting pass")
     ap.add_argument("--png", default="", help="write the assembled image (rank 0)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="debug: gloo runs the N>1 path with host-side collectives and ranks sharing the visible GPUs")
     return ap.parse_args()
 
 
@@ -125,10 +127,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.backend == "gloo":  # rehearsal on fewer GPUs than ranks: ranks share devices
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(a.backend)
     dev = torch.device("cuda", local)
+    cdev = torch.device("cpu") if a.backend == "gloo" else dev  # where collectives run
 
     ctx = rt.Context(local)
     sc = rt.Scene.builtin(a.scene, **scene_assets(a.scene)[0])
@@ -145,7 +150,7 @@ def main():
     max_rows = max(len(x) for x in all_rows)
     fb = torch.empty(a.nfb * len(rows) * a.width * 3, dtype=torch.float32, device=dev)
     img = torch.zeros(max_rows * a.width * 3, dtype=torch.uint8, device=dev)
-    gathered = torch.empty(world * img.numel(), dtype=torch.uint8, device=dev) if world > 1 else None
+    gathered = torch.empty(world * img.numel(), dtype=torch.uint8, device=cdev) if world > 1 else None
 
     stats = None
     if not a.no_stats:  # untimed pass of the counting variant: node / prim tests for B_seg
@@ -163,7 +168,7 @@ def main():
         kms.append(ctx.last_render_ms())
         ctx.resolve(args, fb.data_ptr(), img.data_ptr())
         if world > 1:
-            dist.all_gather_into_tensor(gathered, img)
+            dist.all_gather_into_tensor(gathered, img.to(cdev))
         seg_step[0] = cnt["segments"]
         return cnt
 
@@ -181,8 +186,8 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
 
-    tot = torch.tensor([float(seg_step[0])], dtype=torch.float64, device=dev)
-    tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(seg_step[0])], dtype=torch.float64, device=cdev)
+    tmax = torch.tensor([dt], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)

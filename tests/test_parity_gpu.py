@@ -344,3 +344,27 @@ def test_abi_error_contract(rtlib):
         ctx.render(rtlib.make_args(64, 36, 0), fb.data_ptr())
     ctx.render(args, fb.data_ptr())  # still usable after the failures
     ctx.close()
+
+
+def test_bench_two_ranks_match_one(tmp_path):
+    """bench.py's N>1 path (bands, resolve, all-gather, assembly) as the driver launches it
+    (torch.distributed.run), rehearsed with two ranks on one GPU over gloo: the assembled image
+    is byte-identical to the single-rank run."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["bench.py", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-stats",
+              "--width", "200", "--height", "112", "--spp", "2", "--nfb", "2"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    one = subprocess.run([sys.executable, *common, "--png", str(tmp_path / "n1.png")], cwd=root, env=env,
+                         capture_output=True, text=True, timeout=600)
+    assert one.returncode == 0, one.stderr[-2000:]
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", "29533", *common, "--gpus", "2",
+                          "--backend", "gloo", "--png", str(tmp_path / "n2.png")], cwd=root, env=env,
+                         capture_output=True, text=True, timeout=600)
+    assert two.returncode == 0, two.stderr[-2000:]
+    assert '"n_gpus": 2' in two.stdout
+    assert (tmp_path / "n1.png").read_bytes() == (tmp_path / "n2.png").read_bytes()
