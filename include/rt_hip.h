@@ -170,6 +170,8 @@ enum rt_cam_mode {
                                      log every disagreement (read back with rt_audit_log)       */
 #define RT_FLAG_WIDEST 8          /* testing: run the widest compiled kernel variant that covers
                                      the scene instead of the narrowest (same pixels)           */
+#define RT_FLAG_NO_STEP 16        /* testing: world = one BVH still runs the segment-per-trip
+                                     kernel instead of the stepwise one (same pixels)           */
 
 typedef struct rt_render_args {
   int32_t width, height;  /* full image size; N = width*height drives the RNG slots (H3)  */

@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -57,6 +58,7 @@ enum : int {
   F_EXACT = 1 << 11,  // reference BVH visit set (no culling): node/prim counts equal the oracle's
   F_CHECK = 1 << 12,  // culled search + exact re-run per query; disagreements logged (audit mode)
   F_LDS = 1 << 13,    // BVH nodes + primitives staged in LDS (1024-thread workgroups, 1 per CU)
+  F_STEP = 1 << 14,   // world = one BVH object: render_step_kernel (one traversal step per loop trip)
   F_ALL = (1 << 11) - 2,
   F_SPHERES = F_MOVING | F_CHECKER | F_BVH,           // basic, first, big1 (C2), two_spheres
   F_CORNELL = F_RECT | F_LIST | F_XFORM | F_MEDIUM,   // cornell, cornell_smoke (C3)
@@ -83,7 +85,9 @@ struct DScene {
   int32_t dbg_cap;
   int32_t n_world;
   int32_t lds_nodes;     // F_LDS: node count staged (the primitives follow them)
-  int32_t lds_prims;     // F_LDS: primitive count staged (the traversal stacks follow them)
+  int32_t lds_prims;     // F_LDS: primitive count staged (validation margins follow them)
+  int32_t lds_mats;      // F_LDS: materials staged after the margins (one float4 each)
+  int32_t lds_texs;      // F_LDS: textures staged after the materials (two float4 each; stacks follow)
   rt_camera cam;
   float bg[3];
 };
@@ -114,11 +118,45 @@ __device__ __forceinline__ const float2* pmargin_of(const DScene& S) {
   if constexpr ((F & F_LDS) != 0) return (const float2*)(rt_lds + 2 * S.lds_nodes + 3 * S.lds_prims);
   else return S.pmargin;
 }
+static_assert(sizeof(rt_material) == 16 && sizeof(rt_texture) == 32, "LDS staging copies whole float4s");
+// Materials and textures (F_LDS: staged after the margins; read once per segment by scatter).
+__device__ __forceinline__ int lds_mats_at(const DScene& S) {
+  return 2 * S.lds_nodes + 3 * S.lds_prims + (S.lds_prims + 1) / 2;
+}
 template <int F>
-__device__ __forceinline__ int* stack_of(const DScene& S) {
+__device__ __forceinline__ const int4* mats_of(const DScene& S) {
+  if constexpr ((F & F_LDS) != 0) return (const int4*)(rt_lds + lds_mats_at(S));
+  else return S.mats;
+}
+template <int F>
+__device__ __forceinline__ const rt_texture* texs_of(const DScene& S) {
+  if constexpr ((F & F_LDS) != 0) return (const rt_texture*)(rt_lds + lds_mats_at(S) + S.lds_mats);
+  else return S.texs;
+}
+// Stack entries: child words (pair index, or -1 - primitive).  F_LDS scenes have < 32768 pairs and
+// primitives (they fit in LDS), so their entries are 16-bit (32 KB of stacks per 1024 lanes).
+template <int F>
+using stack_t = std::conditional_t<(F & F_LDS) != 0, short, int>;
+template <int F>
+__device__ __forceinline__ stack_t<F>* stack_of(const DScene& S) {
   if constexpr ((F & F_LDS) != 0)
-    return (int*)(rt_lds + 2 * S.lds_nodes + 3 * S.lds_prims + (S.lds_prims + 1) / 2) + threadIdx.x;
+    return (short*)(rt_lds + lds_mats_at(S) + S.lds_mats + 2 * S.lds_texs) + threadIdx.x;
   else return (int*)rt_lds + threadIdx.x;
+}
+// Stage the read-only scene arrays a F_LDS variant reads in LDS, once per workgroup.
+template <int F>
+__device__ __forceinline__ void stage_lds(const DScene& S) {
+  constexpr int BS = render_block<F>();
+  const int nn = 2 * S.lds_nodes, np = 3 * S.lds_prims, nm = (S.lds_prims + 1) / 2;
+  for (int q = threadIdx.x; q < nn; q += BS) rt_lds[q] = S.nodes[q];
+  for (int q = threadIdx.x; q < np; q += BS) rt_lds[nn + q] = S.prims[q];
+  const float4* pm = (const float4*)S.pmargin;  // padded to an even count at upload
+  for (int q = threadIdx.x; q < nm; q += BS) rt_lds[nn + np + q] = pm[q];
+  const int m0 = nn + np + nm;
+  for (int q = threadIdx.x; q < S.lds_mats; q += BS) rt_lds[m0 + q] = ((const float4*)S.mats)[q];
+  const float4* tx = (const float4*)S.texs;
+  for (int q = threadIdx.x; q < 2 * S.lds_texs; q += BS) rt_lds[m0 + S.lds_mats + q] = tx[q];
+  __syncthreads();
 }
 
 // Per-lane traversal stack in LDS (after the staged scene for F_LDS variants), lane-interleaved
@@ -146,6 +184,23 @@ __device__ __forceinline__ void rt_stamp(int ph) {
 #define RT_STAMP(ph) rt_stamp(ph)
 #else
 #define RT_STAMP(ph)
+#endif
+
+// Diagnostic build only (-DRT_STEP_DIAG): per-wave counts of traversal-loop iterations, lane
+// steps, shading phases and loop trips (render_kernel vs render_step_kernel).
+#ifdef RT_STEP_DIAG
+__device__ unsigned long long rt_diag[4];
+__shared__ unsigned long long rt_diag_acc[16][4];
+__device__ __forceinline__ void rt_diag_wave(int k) {  // one count per wave (first active lane)
+  const unsigned long long act = __ballot(1);
+  if ((int)__lane_id() == __ffsll((long long)act) - 1) {
+    rt_diag_acc[threadIdx.x >> 6][k] += 1;
+    if (k == 0) rt_diag_acc[threadIdx.x >> 6][1] += __popcll(act);
+  }
+}
+#define RT_DIAG(k) rt_diag_wave(k)
+#else
+#define RT_DIAG(k)
 #endif
 
 struct V {
@@ -502,6 +557,135 @@ __device__ bool bvh_exact(const DScene& S, int base, int rows, const Ray& r, V i
   }
 }
 
+// One step of the candidate search of bvh_closest: the node pair of `cur` (one 64-byte record),
+// its primitive children tested right away (leaves hold one primitive), then descend to the nearer
+// hit child (the farther one pushed on the lane's LDS stack) or pop.  Returns false once the
+// search has ended.
+template <int F>
+__device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r, V oi, V finv, float tmin, float tmax,
+                                          int& cur, int& sp, float& best, int& best_prim, int& best_rank,
+                                          bool& overflow, unsigned& nnode, unsigned& nprim) {
+  stack_t<F>* stk = stack_of<F>(S);
+  constexpr int BS = render_block<F>();
+  RT_STAMP(3);
+  const float4* n = nodes_of<F>(S) + 2 * (fb + 2 * cur);
+  const float4 l0 = n[0], l1 = n[1], r0 = n[2], r1 = n[3];
+  if constexpr ((F & F_STATS) != 0) nnode += 2;
+  const float cut = __builtin_fminf(best * 1.00390625f, tmax);
+  float tl, tr;
+  bool hl = fbox(l0, l1, oi, finv, tmin, cut, tl);
+  bool hr = fbox(r0, r1, oi, finv, tmin, cut, tr);
+  const int c0 = __float_as_int(l0.w), c1 = __float_as_int(l1.w);
+  // primitive children are tested right away (leaves hold one primitive)
+  #pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    const int ch = side == 0 ? c0 : c1;
+    if ((side == 0 ? hl : hr) && ch < 0) {
+      RT_STAMP(4);
+      const int pi = -ch - 1;
+      const PrimRec q = load_prim<F>(S, pi);
+      float t;
+      if (prim_t_q<F>(S, q, r, tmin, tmax, t, nprim)) {
+        const int rk = __float_as_int(q.c.y);
+        if (t < best || (t == best && rk < best_rank)) {
+          best = t;
+          best_prim = pi;
+          best_rank = rk;
+        }
+      }
+      if (side == 0) hl = false; else hr = false;
+      RT_STAMP(3);
+    }
+  }
+  if (hl && hr) {
+    const bool right_first = tr < tl;
+    if (sp < kStackDepth) stk[BS * sp++] = (stack_t<F>)(right_first ? c0 : c1);
+    else overflow = true;
+    cur = right_first ? c1 : c0;
+    return true;
+  }
+  if (hl || hr) {
+    cur = hl ? c0 : c1;
+    return true;
+  }
+  if (sp == 0) return false;
+  cur = stk[BS * --sp];
+  return true;
+}
+
+// Second half of bvh_closest once the candidate search has ended: overflow fallback, audit mode,
+// and the reference-chain validation of the candidate (best_rank = its reference leaf rank).
+template <int F>
+__device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, const Ray& r, float tmin, float tmax,
+                                           bool overflow, float& best, int& best_prim, int best_rank, unsigned& nnode,
+                                           unsigned& nprim, unsigned& nfall) {
+  const int last0 = (1 << (rows - 1)) - 1;
+  const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+  if (overflow) {  // a subtree was dropped: answer on the exact visit set instead
+    if constexpr ((F & F_STATS) != 0) ++nfall;
+    return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
+  }
+  if constexpr ((F & F_CHECK) != 0) {
+    float te;
+    int pe;
+    bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, te, pe, nnode, nprim, nfall);
+    if (pe != best_prim || (pe >= 0 && __float_as_uint(te) != __float_as_uint(best))) {
+      const unsigned slot = atomicAdd(S.dbg_n, 1u);
+      if ((int)slot < S.dbg_cap) {
+        float* e = S.dbg + 16 * slot;
+        e[0] = r.o.x; e[1] = r.o.y; e[2] = r.o.z; e[3] = r.d.x; e[4] = r.d.y; e[5] = r.d.z; e[6] = r.tm;
+        e[7] = tmin; e[8] = tmax; e[9] = best; e[10] = __int_as_float(best_prim); e[11] = te;
+        e[12] = __int_as_float(pe); e[13] = __int_as_float(best_rank); e[14] = 0.0f; e[15] = 0.0f;
+      }
+    }
+    best = te;
+    best_prim = pe;
+    return pe >= 0;
+  }
+  if (best_prim < 0) return false;
+  // Reference ancestors whose box contains the winner's box with a margin wider than any
+  // displacement of its computed hit point (hit-distance error up to ~4e-4 t for grazing
+  // spheres, slab rounding 2^-22 of the distance) cannot reject this ray, so only the other
+  // chain positions are tested.  pmargin = {bitmask of chain positions with margin < 0.05,
+  // smallest margin among the rest} (computed at upload).
+  const float dmax = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)),
+                                     __builtin_fabsf(r.d.z));
+  const float bound = 0.001953125f * best * dmax;  // 2^-9 * t * |d|_inf
+  {
+    // Every reference ancestor contains the winner's box, so a computed hit point deeper inside
+    // the winner's own box than `bound` passes all of them: a sphere touches its box only at
+    // six points, so the chain is rarely tested at all.  (Moving spheres: the box at the ray's
+    // time lies inside the box over the shutter.  A negative radius inverts the box: no skip.)
+    const PrimRec q = load_prim<F>(S, best_prim);
+    const int ty = prim_type(q);
+    if (ty == RT_PRIM_SPHERE || ((F & F_MOVING) != 0 && ty == RT_PRIM_MOVING_SPHERE)) {
+      V c = mk(q.a.x, q.a.y, q.a.z);
+      if constexpr ((F & F_MOVING) != 0)
+        if (ty == RT_PRIM_MOVING_SPHERE) c = moving_center(q, r.tm);
+      const V p = r.o + best * r.d;
+      const float rad = q.a.w;
+      const float mx = __builtin_fminf(p.x - (c.x - rad), (c.x + rad) - p.x);
+      const float my = __builtin_fminf(p.y - (c.y - rad), (c.y + rad) - p.y);
+      const float mz = __builtin_fminf(p.z - (c.z - rad), (c.z + rad) - p.z);
+      if (__builtin_fminf(__builtin_fminf(mx, my), mz) > bound) return true;
+    }
+  }
+  const float2 pm = pmargin_of<F>(S)[best_prim];
+  const unsigned must = bound < pm.y ? __float_as_uint(pm.x) : 0xffffffffu;
+  int pos = 0;
+  for (int kr = last0 + (best_rank >> 1);; kr = (kr - 1) >> 1, ++pos) {
+    if ((must >> pos) & 1u) {
+      if constexpr ((F & F_STATS) != 0) ++nnode;
+      const float4 lo = nodes_of<F>(S)[2 * (base + kr)], hi = nodes_of<F>(S)[2 * (base + kr) + 1];
+      if (!box_hit(lo, hi, r, inv, tmin, tmax)) {
+        if constexpr ((F & F_STATS) != 0) ++nfall;
+        return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
+      }
+    }
+    if (kr == 0) return true;
+  }
+}
+
 // Closest primitive of a reference BVH object, same result as bvh_exact.
 //  1. Candidate search on the object's traversal tree (built at upload: same perfect-tree shape,
 //     largest-extent median splits, boxes padded by 2^-16 relative): both children per 64-byte
@@ -521,7 +705,6 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
   if constexpr ((F & F_EXACT) != 0) {
     return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
   } else {
-    const int last0 = (1 << (rows - 1)) - 1;
     const int fb = o.c;  // traversal tree: 64-byte records at nodes[fb + 2i], root i = 0
     // Finite reciprocals for the traversal tree: with d = 0 the fma form would give inf - inf.
     // Clamped to +-1e30 the slab of a parallel axis is (-huge, +huge) inside and empty outside.
@@ -532,119 +715,15 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
     best = __builtin_inff();
     best_prim = -1;
     int best_rank = 0x7fffffff;
-    int* stk = stack_of<F>(S);
-    constexpr int BS = render_block<F>();
     int sp = 0, cur = 0;
     bool overflow = false;
     for (;;) {
-      RT_STAMP(3);
-      const float4* n = nodes_of<F>(S) + 2 * (fb + 2 * cur);
-      const float4 l0 = n[0], l1 = n[1], r0 = n[2], r1 = n[3];
-      if constexpr ((F & F_STATS) != 0) nnode += 2;
-      const float cut = __builtin_fminf(best * 1.00390625f, tmax);
-      float tl, tr;
-      bool hl = fbox(l0, l1, oi, finv, tmin, cut, tl);
-      bool hr = fbox(r0, r1, oi, finv, tmin, cut, tr);
-      const int c0 = __float_as_int(l0.w), c1 = __float_as_int(l1.w);
-      // primitive children are tested right away (leaves hold one primitive)
-      #pragma unroll
-      for (int side = 0; side < 2; ++side) {
-        const int ch = side == 0 ? c0 : c1;
-        if ((side == 0 ? hl : hr) && ch < 0) {
-          RT_STAMP(4);
-          const int pi = -ch - 1;
-          const PrimRec q = load_prim<F>(S, pi);
-          float t;
-          if (prim_t_q<F>(S, q, r, tmin, tmax, t, nprim)) {
-            const int rk = __float_as_int(q.c.y);
-            if (t < best || (t == best && rk < best_rank)) {
-              best = t;
-              best_prim = pi;
-              best_rank = rk;
-            }
-          }
-          if (side == 0) hl = false; else hr = false;
-          RT_STAMP(3);
-        }
-      }
-      if (hl && hr) {
-        const bool right_first = tr < tl;
-        if (sp < kStackDepth) stk[BS * sp++] = right_first ? c0 : c1;
-        else overflow = true;
-        cur = right_first ? c1 : c0;
-        continue;
-      }
-      if (hl || hr) {
-        cur = hl ? c0 : c1;
-        continue;
-      }
-      if (sp == 0) break;
-      cur = stk[BS * --sp];
+      RT_DIAG(0);
+      if (!trav_step<F>(S, fb, r, oi, finv, tmin, tmax, cur, sp, best, best_prim, best_rank, overflow, nnode, nprim))
+        break;
     }
     RT_STAMP(5);
-    if (overflow) {  // a subtree was dropped: answer on the exact visit set instead
-      if constexpr ((F & F_STATS) != 0) ++nfall;
-      return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
-    }
-    if constexpr ((F & F_CHECK) != 0) {
-      float te;
-      int pe;
-      bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, te, pe, nnode, nprim, nfall);
-      if (pe != best_prim || (pe >= 0 && __float_as_uint(te) != __float_as_uint(best))) {
-        const unsigned slot = atomicAdd(S.dbg_n, 1u);
-        if ((int)slot < S.dbg_cap) {
-          float* e = S.dbg + 16 * slot;
-          e[0] = r.o.x; e[1] = r.o.y; e[2] = r.o.z; e[3] = r.d.x; e[4] = r.d.y; e[5] = r.d.z; e[6] = r.tm;
-          e[7] = tmin; e[8] = tmax; e[9] = best; e[10] = __int_as_float(best_prim); e[11] = te;
-          e[12] = __int_as_float(pe); e[13] = __int_as_float(best_rank); e[14] = 0.0f; e[15] = 0.0f;
-        }
-      }
-      best = te;
-      best_prim = pe;
-      return pe >= 0;
-    }
-    if (best_prim < 0) return false;
-    // Reference ancestors whose box contains the winner's box with a margin wider than any
-    // displacement of its computed hit point (hit-distance error up to ~4e-4 t for grazing
-    // spheres, slab rounding 2^-22 of the distance) cannot reject this ray, so only the other
-    // chain positions are tested.  pmargin = {bitmask of chain positions with margin < 0.05,
-    // smallest margin among the rest} (computed at upload).
-    const float dmax = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)),
-                                       __builtin_fabsf(r.d.z));
-    const float bound = 0.001953125f * best * dmax;  // 2^-9 * t * |d|_inf
-    {
-      // Every reference ancestor contains the winner's box, so a computed hit point deeper inside
-      // the winner's own box than `bound` passes all of them: a sphere touches its box only at
-      // six points, so the chain is rarely tested at all.  (Moving spheres: the box at the ray's
-      // time lies inside the box over the shutter.  A negative radius inverts the box: no skip.)
-      const PrimRec q = load_prim<F>(S, best_prim);
-      const int ty = prim_type(q);
-      if (ty == RT_PRIM_SPHERE || ((F & F_MOVING) != 0 && ty == RT_PRIM_MOVING_SPHERE)) {
-        V c = mk(q.a.x, q.a.y, q.a.z);
-        if constexpr ((F & F_MOVING) != 0)
-          if (ty == RT_PRIM_MOVING_SPHERE) c = moving_center(q, r.tm);
-        const V p = r.o + best * r.d;
-        const float rad = q.a.w;
-        const float mx = __builtin_fminf(p.x - (c.x - rad), (c.x + rad) - p.x);
-        const float my = __builtin_fminf(p.y - (c.y - rad), (c.y + rad) - p.y);
-        const float mz = __builtin_fminf(p.z - (c.z - rad), (c.z + rad) - p.z);
-        if (__builtin_fminf(__builtin_fminf(mx, my), mz) > bound) return true;
-      }
-    }
-    const float2 pm = pmargin_of<F>(S)[best_prim];
-    const unsigned must = bound < pm.y ? __float_as_uint(pm.x) : 0xffffffffu;
-    int pos = 0;
-    for (int kr = last0 + (best_rank >> 1);; kr = (kr - 1) >> 1, ++pos) {
-      if ((must >> pos) & 1u) {
-        if constexpr ((F & F_STATS) != 0) ++nnode;
-        const float4 lo = nodes_of<F>(S)[2 * (base + kr)], hi = nodes_of<F>(S)[2 * (base + kr) + 1];
-        if (!box_hit(lo, hi, r, inv, tmin, tmax)) {
-          if constexpr ((F & F_STATS) != 0) ++nfall;
-          return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
-        }
-      }
-      if (kr == 0) return true;
-    }
+    return bvh_settle<F>(S, base, rows, r, tmin, tmax, overflow, best, best_prim, best_rank, nnode, nprim, nfall);
   }
 }
 
@@ -832,10 +911,10 @@ __device__ V tex_leaf(const DScene& S, const rt_texture& T, float u, float v, V 
 }
 template <int F>
 __device__ V tex_value(const DScene& S, int ti, float u, float v, V p) {
-  const rt_texture T = S.texs[ti];
+  const rt_texture T = texs_of<F>(S)[ti];
   if constexpr ((F & F_CHECKER) != 0) {
     if (T.type == RT_TEX_CHECKER) {  // texture.h:37-45: sin(10x) sin(10y) sin(10z) < 0 -> odd
-      return tex_leaf<F>(S, S.texs[rtm::checker_odd(10.0f * p.x, 10.0f * p.y, 10.0f * p.z) ? T.b : T.a], u, v, p);
+      return tex_leaf<F>(S, texs_of<F>(S)[rtm::checker_odd(10.0f * p.x, 10.0f * p.y, 10.0f * p.z) ? T.b : T.a], u, v, p);
     }
   }
   return tex_leaf<F>(S, T, u, v, p);
@@ -845,7 +924,7 @@ __device__ V tex_value(const DScene& S, int ti, float u, float v, V p) {
 // Returns true when the path continues (att, scattered set).  em = emitted colour.
 template <int F>
 __device__ bool scatter(const DScene& S, const Ray& in, const Hit& h, V& att, Ray& out, V& em, Rng& rng) {
-  const int4 m = S.mats[h.mat];
+  const int4 m = mats_of<F>(S)[h.mat];
   const int mt = m.x;
   em = mk(0.0f, 0.0f, 0.0f);
   // lambertian, metal and isotropic each draw exactly one random_in_unit_sphere and nothing else
@@ -916,7 +995,8 @@ struct RenderParams {
   unsigned long long total_items;
   long long npix;  // W*H of the full image
   int W, H, rows, spp, fb_first, max_depth, cam_mode, fb_count;
-  int pad3, pad4;
+  int shade_min;  // render_step_kernel: lanes waiting before a wave runs its shading phase
+  int pad4;
   uint32_t cam_state[6];
 #ifdef RT_TRACE
   float* trace;
@@ -930,9 +1010,34 @@ struct RenderParams {
 constexpr int kBlock = 256;
 constexpr int kAuditCap = 4096;
 constexpr int kRefill = 16;  // refill a wave once this many lanes are idle
+constexpr int kShadeMin = 60;  // render_step_kernel: default shading-phase threshold
+constexpr unsigned kChunk = 64;  // items a wave claims per work-counter atomic
 
 __device__ __forceinline__ unsigned lane_rank(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+
+// Work items for the lanes in `idle` (lane order) from the wave's chunk [chunk_base, +chunk_left)
+// of the global work counter; a chunk of kChunk items is claimed with ONE atomic when the current
+// one runs short (all waves of the grid hit one counter: its atomics serialise in L2).
+__device__ __forceinline__ unsigned long long claim_items(unsigned long long* work, unsigned long long idle,
+                                                          unsigned long long& chunk_base, unsigned& chunk_left) {
+  const unsigned nidle = (unsigned)__popcll(idle);
+  const unsigned long long old_base = chunk_base;
+  const unsigned old_left = chunk_left;
+  unsigned long long fresh = 0;
+  if (old_left < nidle) {
+    const int leader = __ffsll((long long)idle) - 1;
+    if ((int)__lane_id() == leader) fresh = atomicAdd(work, (unsigned long long)kChunk);
+    fresh = __shfl(fresh, leader, 64);
+    chunk_base = fresh + (nidle - old_left);
+    chunk_left = kChunk - (nidle - old_left);
+  } else {
+    chunk_base = old_base + nidle;
+    chunk_left = old_left - nidle;
+  }
+  const unsigned rk = lane_rank(idle);
+  return rk < old_left ? old_base + rk : fresh + (rk - old_left);
 }
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
@@ -943,16 +1048,11 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 template <int F>
 __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderParams P) {
   const DScene& S = P.S;
-  if constexpr ((F & F_LDS) != 0) {
-    // Stage nodes and primitives (read-only, scene-sized) in LDS once per workgroup.
-    const int nn = 2 * P.S.lds_nodes, np = 3 * P.S.lds_prims, nm = (P.S.lds_prims + 1) / 2;
-    for (int q = threadIdx.x; q < nn; q += render_block<F>()) rt_lds[q] = P.S.nodes[q];
-    for (int q = threadIdx.x; q < np; q += render_block<F>()) rt_lds[nn + q] = P.S.prims[q];
-    const float4* pm = (const float4*)P.S.pmargin;  // padded to an even count at upload
-    for (int q = threadIdx.x; q < nm; q += render_block<F>()) rt_lds[nn + np + q] = pm[q];
-    __syncthreads();
-  }
+  if constexpr ((F & F_LDS) != 0) stage_lds<F>(S);  // nodes, primitives, margins, materials, textures
   const unsigned lane = __lane_id();
+#ifdef RT_STEP_DIAG
+  if (lane < 4) rt_diag_acc[threadIdx.x >> 6][lane] = 0;
+#endif
 #ifdef RT_STAMPS
   if (lane < kStampPhases + 2) rt_stamp_acc[threadIdx.x >> 6][lane] = 0;
   __syncthreads();
@@ -969,6 +1069,8 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
   unsigned nnode = 0, nprim = 0, nfall = 0;
   const bool per_pixel = P.cam_mode == RT_CAM_PER_PIXEL;
   const rt_camera& C = S.cam;
+  unsigned long long chunk_base = 0;  // wave-uniform: next unclaimed item of the wave's chunk
+  unsigned chunk_left = 0;
 
   for (;;) {
     // ---- refill idle lanes (one atomic per wave, ballot-compacted ranks)
@@ -978,12 +1080,8 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
     const unsigned long long busy = __ballot(item >= 0);
     const int nidle = __popcll(idle);
     if (nidle > 0 && (nidle >= kRefill || busy == 0)) {
-      const int leader = __ffsll((long long)idle) - 1;
-      unsigned long long base = 0;
-      if ((int)lane == leader) base = atomicAdd(P.work, (unsigned long long)nidle);
-      base = __shfl(base, leader, 64);
+      const unsigned long long mine = claim_items(P.work, idle, chunk_base, chunk_left);
       if (item < 0 && !done) {
-        const unsigned long long mine = base + lane_rank(idle);
         if (mine >= P.total_items) {
           done = true;
         } else {
@@ -1041,6 +1139,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
       const unsigned rng_in = loc.d;
   #endif
       RT_STAMP(2);
+      RT_DIAG(2);
       const bool hit_any = world_hit<F>(S, ray, h, loc, nnode, nprim, nfall);
       RT_STAMP(6);
   #ifdef RT_TRACE
@@ -1093,6 +1192,188 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
 #ifdef RT_STAMPS
   RT_STAMP(0);
   if (lane < kStampPhases) atomicAdd(P.stamps + lane, rt_stamp_acc[threadIdx.x >> 6][2 + lane]);
+#endif
+#ifdef RT_STEP_DIAG
+  if (lane < 4) atomicAdd(&rt_diag[lane], rt_diag_acc[threadIdx.x >> 6][lane]);
+#endif
+  const unsigned long long ws = wave_sum(nseg), wm = wave_sum(nsamp);
+  unsigned long long wn = 0, wp = 0, wf = 0;
+  if constexpr ((F & F_STATS) != 0) {
+    wn = wave_sum(nnode);
+    wp = wave_sum(nprim);
+    wf = wave_sum(nfall);
+  }
+  if (lane == 0) {
+    atomicAdd(&P.counters[0], ws);
+    atomicAdd(&P.counters[3], wm);
+    if constexpr ((F & F_STATS) != 0) {
+      atomicAdd(&P.counters[1], wn);
+      atomicAdd(&P.counters[2], wp);
+      atomicAdd(&P.counters[4], wf);
+    }
+  }
+}
+
+// Stepwise megakernel for worlds that are ONE BVH object (C1/C2 sphere scenes).  render_kernel
+// runs a whole world query per loop trip, so every lane of a wave stays in the traversal until
+// the wave's longest query ends (~27 % lane utilisation on C2).  Here one loop trip is ONE
+// traversal step (trav_step: a node pair and its primitive leaves) for the lanes that are
+// traversing; a lane whose search has ended waits, and once `shade_min` lanes wait (or none is
+// traversing) the wave runs its shading phase for all of them together: validation + hit record
+// (bvh_settle, finalize), scatter, sample / item bookkeeping, refill from the work counter,
+// the next camera ray and the next query's setup.  Per lane the sequence of RNG draws and float
+// operations is exactly render_kernel's, so frame buffers are bit-identical.
+template <int F>
+__global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const RenderParams P) {
+  const DScene& S = P.S;
+  if constexpr ((F & F_LDS) != 0) stage_lds<F>(S);  // nodes, primitives, margins, materials, textures
+  const unsigned lane = __lane_id();
+#ifdef RT_STEP_DIAG
+  if (lane < 4) rt_diag_acc[threadIdx.x >> 6][lane] = 0;
+#endif
+  const rt_object obj = S.objects[S.world[0]];
+  const int tbase = obj.c;  // traversal tree of the world's BVH
+  const float tmin = 0.001f, tmax = __builtin_inff();  // render.h:63
+  long long item = -1;  // -1: no item
+  bool done = false;
+  int mode = 0;  // 0: between queries, 1: traversing, 2: search ended, shading pending
+  int f = 0, i = 0, r = 0, j = 0, s = 0, depth = 0;
+  Rng loc{}, cam{};
+  Ray ray{};
+  V att = mk(1, 1, 1), col = mk(0, 0, 0);
+  V finv = mk(0, 0, 0), oi = mk(0, 0, 0);
+  int cur = 0, sp = 0, best_prim = -1, best_rank = 0x7fffffff;
+  float best = 0.0f;
+  bool overflow = false;
+  unsigned nseg = 0, nsamp = 0, item_segs = 0;
+  unsigned nnode = 0, nprim = 0, nfall = 0;
+  const bool per_pixel = P.cam_mode == RT_CAM_PER_PIXEL;
+  const rt_camera& C = S.cam;
+  unsigned long long chunk_base = 0;  // wave-uniform: next unclaimed item of the wave's chunk
+  unsigned chunk_left = 0;
+
+  for (;;) {
+    {
+      RT_DIAG(2);
+      // ---- shading phase: finish the ended queries (render.h:60-77)
+      if (mode == 2) {
+        ++nseg;
+        ++item_segs;
+        bool ended = false;
+        V contrib;
+        if (!bvh_settle<F>(S, obj.a, obj.b, ray, tmin, tmax, overflow, best, best_prim, best_rank, nnode, nprim,
+                           nfall)) {
+          contrib = att * ld3(S.bg);
+          ended = true;
+        } else {
+          Hit h;
+          finalize<F>(S, best_prim, ray, tmin, best, h);
+          V a, em;
+          Ray sc;
+          if (scatter<F>(S, ray, h, a, sc, em, loc)) {
+            att = att * a;
+            ray = sc;
+            if (++depth == P.max_depth) {
+              contrib = mk(0.0f, 0.0f, 0.0f);
+              ended = true;
+            }
+          } else {
+            contrib = att * em;
+            ended = true;
+          }
+        }
+        if (ended) {
+          col = col + contrib;
+          depth = 0;
+          ++nsamp;
+          if (++s == P.spp) {
+            const V out = (1.0f / (float)P.spp) * col;
+            float* dst = P.fb + 3 * (((long long)f * P.rows + r) * P.W + i);
+            dst[0] = out.x;
+            dst[1] = out.y;
+            dst[2] = out.z;
+            if (P.row_cost && (i & 15) == 0) atomicAdd(&P.row_cost[j], (unsigned long long)item_segs);
+            item = -1;
+          }
+        }
+        mode = 0;
+      }
+      // ---- refill lanes without an item from the wave's chunk of the work counter (one atomic
+      // per kChunk items: a single counter serialises its atomics in L2)
+      const unsigned long long idle = __ballot(item < 0 && !done);
+      if (idle != 0) {
+        const unsigned long long mine = claim_items(P.work, idle, chunk_base, chunk_left);
+        if (item < 0 && !done) {
+          if (mine >= P.total_items) {
+            done = true;
+          } else {
+            item = (long long)mine;
+            const long long per_row = (long long)P.fb_count * P.W;  // same item order as render_kernel
+            const int q = (int)(item / per_row);
+            const long long rem = item - (long long)q * per_row;
+            r = P.row_order[q];
+            f = (int)(rem / P.W);
+            i = (int)(rem - (long long)f * P.W);
+            j = P.row_map[r];
+            const long long id = P.fb_first + f;
+            const long long p = (long long)j * P.W + i;
+            const long long slot = ((id + 1) * p + id + 1) % P.npix;  // render.h:101 (H3)
+            const uint4 s0 = P.states[2 * slot], s1 = P.states[2 * slot + 1];
+            loc.d = s0.x; loc.v[0] = s0.y; loc.v[1] = s0.z; loc.v[2] = s0.w; loc.v[3] = s1.x; loc.v[4] = s1.y;
+            s = 0;
+            depth = 0;
+            item_segs = 0;
+            col = mk(0, 0, 0);
+          }
+        }
+      }
+      // ---- next query: camera ray at a sample's start (render.h:105-108, camera.h:49-58)
+      if (item >= 0 && mode == 0) {
+        if (depth == 0) {
+          if (s == 0) {
+            cam.d = P.cam_state[0];
+            for (int k = 0; k < 5; ++k) cam.v[k] = P.cam_state[1 + k];
+          }
+          const float u = ((float)i + rtx::uniform(loc)) / (float)P.W;
+          const float v = ((float)j + rtx::uniform(loc)) / (float)P.H;
+          Rng& cr = per_pixel ? loc : cam;
+          const V rd = C.lens_radius * in_unit_disk(cr);
+          const V off = rd.x * ld3(C.u) + rd.y * ld3(C.v);
+          ray.o = ld3(C.origin) + off;
+          ray.d = ld3(C.lower_left) + u * ld3(C.horizontal) + v * ld3(C.vertical) - ld3(C.origin) - off;
+          ray.tm = urange(cr, C.time0, C.time1);
+          att = mk(1.0f, 1.0f, 1.0f);
+        }
+        const V inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+        finv = mk(__builtin_fminf(__builtin_fmaxf(inv.x, -1e30f), 1e30f),
+                  __builtin_fminf(__builtin_fmaxf(inv.y, -1e30f), 1e30f),
+                  __builtin_fminf(__builtin_fmaxf(inv.z, -1e30f), 1e30f));
+        oi = mk(ray.o.x * finv.x, ray.o.y * finv.y, ray.o.z * finv.z);
+        best = __builtin_inff();
+        best_prim = -1;
+        best_rank = 0x7fffffff;
+        cur = 0;
+        sp = 0;
+        overflow = false;
+        mode = 1;
+      }
+    }
+    if (__ballot(mode == 1) == 0) break;  // no item left for any lane of the wave
+    // ---- traversal steps until shade_min lanes wait (or none traverses)
+    for (;;) {
+      RT_DIAG(3);
+      if (mode == 1) {
+        RT_DIAG(0);
+        if (!trav_step<F>(S, tbase, ray, oi, finv, tmin, tmax, cur, sp, best, best_prim, best_rank, overflow, nnode,
+                          nprim))
+          mode = 2;
+      }
+      if (__ballot(mode == 1) == 0 || __popcll(__ballot(mode == 2)) >= P.shade_min) break;
+    }
+  }
+
+#ifdef RT_STEP_DIAG
+  if (lane < 4) atomicAdd(&rt_diag[lane], rt_diag_acc[threadIdx.x >> 6][lane]);
 #endif
   const unsigned long long ws = wave_sum(nseg), wm = wave_sum(nsamp);
   unsigned long long wn = 0, wp = 0, wf = 0;
@@ -1193,9 +1474,10 @@ struct rt_ctx {
   std::vector<unsigned long long> host_cost;
   long long cost_key[5] = {-1, -1, -1, -1, -1};
   long long scene_gen = 0;
-  int cus = 0, blocks_per_cu[16] = {0};
+  int cus = 0, blocks_per_cu[32] = {0};  // per kernel variant (kVariants)
   int features = 0;
-  int dev_nodes = 0, dev_prims = 0;  // device array sizes (for LDS staging)
+  bool world_bvh = false;  // the world list is one BVH object (render_step_kernel applies)
+  int dev_nodes = 0, dev_prims = 0, dev_mats = 0, dev_texs = 0;  // device array sizes (for LDS staging)
   float last_ms = 0.0f;
   float* dbg = nullptr;  // audit log: [0] = count, then 16 floats per entry
 };
@@ -1207,7 +1489,10 @@ struct Variant {
   const void* fn;
 };
 #define RT_VARIANT(m) {m, (const void*)render_kernel<m>}
+#define RT_VARIANT_STEP(m) {m, (const void*)render_step_kernel<m>}
 const Variant kVariants[] = {
+    RT_VARIANT_STEP(F_SPHERES | F_LDS | F_STEP),
+    RT_VARIANT_STEP(F_SPHERES | F_STEP),
     RT_VARIANT(F_SPHERES),
     RT_VARIANT(F_ALL),
     RT_VARIANT(F_SPHERES | F_STATS),
@@ -1228,12 +1513,14 @@ const Variant kVariants[] = {
     RT_VARIANT(F_MESH | F_EXACT),
 };
 #undef RT_VARIANT
-constexpr int kNumVariants = 18;
+#undef RT_VARIANT_STEP
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+static_assert(kNumVariants <= 32, "rt_ctx::blocks_per_cu holds 32 variants");
 constexpr int kLdsBudget = 156 * 1024;  // bytes of staged nodes + primitives + stacks per workgroup
 
 // Smallest compiled variant that covers the scene's features and the requested mode.
-int pick_variant(int features, bool stats, bool exact, bool check, bool lds, bool widest = false) {
-  const int modes = F_STATS | F_EXACT | F_CHECK | F_LDS;
+int pick_variant(int features, bool stats, bool exact, bool check, bool lds, bool widest = false, bool step = false) {
+  const int modes = F_STATS | F_EXACT | F_CHECK | F_LDS | F_STEP;
   const int mode = check ? F_CHECK : ((stats ? F_STATS : 0) | (exact ? F_EXACT : 0));
   auto best_of = [&](int want) {  // covering variant with the fewest (widest: most) feature bits
     int best = -1;
@@ -1245,10 +1532,16 @@ int pick_variant(int features, bool stats, bool exact, bool check, bool lds, boo
     }
     return best;
   };
-  const int v = best_of(mode);
+  int v = best_of(mode);
   if (v >= 0 && lds && mode == 0)  // the LDS twin of that variant, when one is compiled
     for (int w = 0; w < kNumVariants; ++w)
-      if (kVariants[w].mask == (kVariants[v].mask | F_LDS)) return w;
+      if (kVariants[w].mask == (kVariants[v].mask | F_LDS)) {
+        v = w;
+        break;
+      }
+  if (v >= 0 && step && mode == 0)  // its stepwise twin (world = one BVH object)
+    for (int w = 0; w < kNumVariants; ++w)
+      if (kVariants[w].mask == (kVariants[v].mask | F_STEP)) return w;
   return v;
 }
 int variant_block(int v) { return (kVariants[v].mask & F_LDS) != 0 ? 1024 : 256; }
@@ -1618,8 +1911,11 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   d.bg[1] = s->background[1];
   d.bg[2] = s->background[2];
   c->features = scene_features(s);
+  c->world_bvh = s->n_world == 1 && s->objects[s->world[0]].kind == RT_OBJ_BVH;
   c->dev_nodes = (int)nodes.size();
   c->dev_prims = (int)prims.size();
+  c->dev_mats = s->n_materials;
+  c->dev_texs = s->n_textures;
   c->have_scene = true;
   return RT_OK;
 }
@@ -1710,10 +2006,16 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
 
   const bool stats = a->stats != 0;
   const bool check = (a->flags & RT_FLAG_AUDIT) != 0;
-  const size_t lds_bytes = (size_t)(2 * c->dev_nodes + 3 * c->dev_prims + (c->dev_prims + 1) / 2) * sizeof(float4);
-  const bool use_lds = lds_bytes + 1024 * kStackDepth * 4 <= (size_t)kLdsBudget && (a->flags & RT_FLAG_NO_LDS) == 0;
+  const size_t lds_bytes =
+      (size_t)(2 * c->dev_nodes + 3 * c->dev_prims + (c->dev_prims + 1) / 2 + c->dev_mats + 2 * c->dev_texs) * sizeof(float4);
+  const bool use_lds = lds_bytes + 1024 * kStackDepth * 2 <= (size_t)kLdsBudget && c->dev_nodes / 2 < 32768 &&
+                       c->dev_prims < 32768 && (a->flags & RT_FLAG_NO_LDS) == 0;
+  const bool step = c->world_bvh && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
   const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
-                               (a->flags & RT_FLAG_WIDEST) != 0);
+                               (a->flags & RT_FLAG_WIDEST) != 0, step);
+  // shading phase of render_step_kernel once this many lanes of a wave wait (RT_SHADE_MIN: tuning)
+  P.shade_min = kShadeMin;
+  if (const char* e = getenv("RT_SHADE_MIN")) P.shade_min = std::max(1, std::min(64, atoi(e)));
   if (check) {
     if (!c->dbg) {
       HIPCHK(c, hipMalloc((void**)&c->dbg, 16 * sizeof(float) * kAuditCap + 64));
@@ -1728,7 +2030,9 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   const bool lds_var = (kVariants[var].mask & F_LDS) != 0;
   P.S.lds_nodes = lds_var ? c->dev_nodes : 0;
   P.S.lds_prims = lds_var ? c->dev_prims : 0;
-  const size_t shmem = (lds_var ? lds_bytes : 0) + (size_t)bs * kStackDepth * 4;
+  P.S.lds_mats = lds_var ? c->dev_mats : 0;
+  P.S.lds_texs = lds_var ? c->dev_texs : 0;
+  const size_t shmem = lds_var ? lds_bytes + (size_t)bs * kStackDepth * 2 : (size_t)bs * kStackDepth * 4;
   const long long resident = (long long)c->cus * std::max(1, c->blocks_per_cu[var]);
   // Persistent grid: every resident workgroup, even when there are fewer items than lanes (a
   // rank of a multi-GPU run): waves take items dynamically, so the items spread over all CUs
@@ -1752,6 +2056,12 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   hipMemsetAsync(tbuf, 0, 16 * 256 * sizeof(float), c->stream);
   P.trace = getenv("RT_TRACE_ITEM") ? tbuf : nullptr;
   P.trace_item = getenv("RT_TRACE_ITEM") ? atoll(getenv("RT_TRACE_ITEM")) : -1;
+#endif
+#ifdef RT_STEP_DIAG
+  {
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    hipMemcpyToSymbol(HIP_SYMBOL(rt_diag), z, sizeof(z));
+  }
 #endif
   void* kargs[] = {&P};
   HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), kargs, shmem, c->stream));
@@ -1777,6 +2087,14 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
     counters->samples = host_cnt[4];
     counters->fallbacks = host_cnt[5];
   }
+#ifdef RT_STEP_DIAG
+  {
+    unsigned long long h[4];
+    hipMemcpyFromSymbol(h, HIP_SYMBOL(rt_diag), sizeof(h));
+    fprintf(stderr, "RT_STEP_DIAG var=%d trav_wave_iters=%llu trav_lane_steps=%llu shade_phases=%llu trips=%llu\n", var,
+            h[0], h[1], h[2], h[3]);
+  }
+#endif
 #ifdef RT_STAMPS
   if (getenv("RT_STAMPS_OUT")) {
     unsigned long long hs[8];

@@ -28,17 +28,17 @@ SMALL = [
 ]
 
 
-def _gpu_render(rt, ctx, scene, W, H, spp, fb_first, fb_count, cam, depth=50, band=None, exact=False):
+def _gpu_render(rt, ctx, scene, W, H, spp, fb_first, fb_count, cam, depth=50, band=None, exact=False, step=True):
     import torch
 
     sc = rt.Scene.builtin(scene)
     ctx.upload(sc)
     ctx.render_init(W, H, 1984)
     if band is None:
-        args = rt.make_args(W, H, spp, fb_first, fb_count, depth, cam, exact=exact)
+        args = rt.make_args(W, H, spp, fb_first, fb_count, depth, cam, exact=exact, step=step)
     else:
         args = rt.make_args(W, H, spp, fb_first, fb_count, depth, cam, band_rows=band[0], band_first=band[1],
-                            band_stride=band[2], exact=exact)
+                            band_stride=band[2], exact=exact, step=step)
     rows = rt.owned_rows(args)
     fb = torch.zeros(fb_count * len(rows) * W * 3, dtype=torch.float32, device="cuda")
     cnt = ctx.render(args, fb.data_ptr())
@@ -258,6 +258,26 @@ def test_culled_equals_exact_full_workload(rtlib, gpu_ctx, scene, W, H, spp, nfb
     ex, _, ce, _, _ = _gpu_render(rtlib, gpu_ctx, scene, W, H, spp, 0, nfb, REF, exact=True)
     assert cf["segments"] == ce["segments"]
     assert np.array_equal(_bits(fast), _bits(ex))
+
+
+@pytest.mark.parametrize("scene,W,H,spp,nfb,cam", [
+    ("big1", 1200, 800, 10, 10, REF),     # the whole C2 bench workload
+    ("big1", 333, 187, 3, 2, PIX),
+    ("basic", 200, 100, 4, 2, REF),
+    ("first", 160, 90, 4, 2, REF),
+])
+def test_step_kernel_equals_segment_loop(rtlib, gpu_ctx, oracle, scene, W, H, spp, nfb, cam):
+    """render_step_kernel (one traversal step per loop trip, batched shading; the default for
+    worlds that are one BVH) gives every float of the segment-per-trip kernel, same segments."""
+    a, _, ca, _, _ = _gpu_render(rtlib, gpu_ctx, scene, W, H, spp, 0, nfb, cam)
+    b, _, cb, _, _ = _gpu_render(rtlib, gpu_ctx, scene, W, H, spp, 0, nfb, cam, step=False)
+    assert ca["segments"] == cb["segments"] and ca["samples"] == cb["samples"]
+    assert np.array_equal(_bits(a), _bits(b))
+    if W * H * spp <= 20000:
+        ref = oracle.RefScene(scene)
+        for f in range(nfb):
+            want, _, _ = ref.render(W, H, spp, f, 50, cam)
+            assert np.array_equal(_bits(a[f]), _bits(want.reshape(H, W, 3)))
 
 
 @pytest.mark.parametrize("key,scene,W,H,spp,fbs,depth", [
