@@ -163,11 +163,13 @@ def main():
 
     seg_step = [0]
     kms = []
+    kname = [""]
 
     def step():
         ctx.render_init(a.width, a.height, 1984)
         cnt = ctx.render(args, fb.data_ptr())
         kms.append(ctx.last_render_ms())
+        kname[0] = ctx.last_render_kernel()
         ctx.resolve(args, fb.data_ptr(), img.data_ptr())
         if world > 1:
             dist.all_gather_into_tensor(gathered, img.to(cdev))
@@ -209,7 +211,7 @@ def main():
             achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                    "kernel": "render_kernel", "kernel_avg_ms": round(avg_ms, 3),
+                    "kernel": kname[0], "kernel_avg_ms": round(avg_ms, 3),
                     "bytes_per_launch": int(bytes_launch),
                     "bytes_per_segment": round(bytes_launch / max(stats["segments"], 1), 2),
                     "node_tests_per_segment": round(stats["node_tests"] / max(stats["segments"], 1), 3),

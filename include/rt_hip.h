@@ -220,6 +220,9 @@ int rt_read_states(rt_ctx* ctx, int64_t first, int64_t count, uint32_t* out);
 int rt_render(rt_ctx* ctx, const rt_render_args* args, float* fb_dev, rt_counters* counters);
 /* Duration in ms of the last render kernel, from HIP events recorded on the context stream. */
 float rt_last_render_ms(const rt_ctx* ctx);
+/* Kernel of the last render launch as rocprof names it (stem, e.g. "render_step_kernel<25730>"):
+ * the kernel variant the context picked for the scene's features and flags. */
+const char* rt_last_render_kernel(const rt_ctx* ctx);
 /* Audit log of the last RT_FLAG_AUDIT render: 16 floats per disagreeing BVH query (ray o[3] d[3]
  * time, tmin, tmax, culled t, culled prim (int bits), exact t, exact prim, culled rank, 0, 0).
  * Copies up to cap entries into out (may be NULL); returns the total number of disagreements. */

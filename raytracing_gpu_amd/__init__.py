@@ -108,6 +108,7 @@ ABI = {
     "rt_read_states": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
     "rt_render": (c_int, [c_void_p, POINTER(rt_render_args), c_void_p, POINTER(rt_counters)]),
     "rt_last_render_ms": (c_float, [c_void_p]),
+    "rt_last_render_kernel": (ctypes.c_char_p, [c_void_p]),
     "rt_audit_log": (c_int, [c_void_p, POINTER(c_float), c_int32]),
     "rt_resolve": (c_int, [c_void_p, POINTER(rt_render_args), c_void_p, c_void_p]),
     "rt_draw": (c_int, [c_void_p, POINTER(rt_render_args), POINTER(c_uint8), POINTER(rt_counters)]),
@@ -299,6 +300,10 @@ class Context:
 
     def last_render_ms(self) -> float:
         return float(lib().rt_last_render_ms(self._c))
+
+    def last_render_kernel(self) -> str:
+        """rocprof name stem of the kernel the last render launched."""
+        return lib().rt_last_render_kernel(self._c).decode()
 
     def audit_log(self, cap: int = 4096) -> tuple[int, np.ndarray]:
         """(number of disagreements, [min(n, cap), 16] float32 entries) of the last audit render."""

@@ -378,9 +378,12 @@ __device__ __forceinline__ bool prim_t_q(const DScene& S, const PrimRec& q, cons
                                          float& t, unsigned& nprim) {
   if constexpr ((F & F_STATS) != 0) ++nprim;
   const int type = prim_type(q);
-  if (type == RT_PRIM_SPHERE) return sphere_t(r, mk(q.a.x, q.a.y, q.a.z), q.a.w, tmin, tmax, t);
-  if constexpr ((F & F_MOVING) != 0)
-    if (type == RT_PRIM_MOVING_SPHERE) return sphere_t(r, moving_center(q, r.tm), q.a.w, tmin, tmax, t);
+  if (type <= RT_PRIM_MOVING_SPHERE) {  // one quadratic for both sphere kinds (lanes of a wave mix them)
+    V c = mk(q.a.x, q.a.y, q.a.z);
+    if constexpr ((F & F_MOVING) != 0)
+      if (type == RT_PRIM_MOVING_SPHERE) c = moving_center(q, r.tm);
+    return sphere_t(r, c, q.a.w, tmin, tmax, t);
+  }
   if constexpr ((F & F_TRI) != 0)
     if (type == RT_PRIM_TRIANGLE) return tri_t(r, q, tmin, tmax, t);
   if constexpr ((F & F_RECT) != 0) {
@@ -1479,6 +1482,7 @@ struct rt_ctx {
   bool world_bvh = false;  // the world list is one BVH object (render_step_kernel applies)
   int dev_nodes = 0, dev_prims = 0, dev_mats = 0, dev_texs = 0;  // device array sizes (for LDS staging)
   float last_ms = 0.0f;
+  char last_kernel[48] = "";  // rocprof name stem of the last render launch, e.g. render_step_kernel<25730>
   float* dbg = nullptr;  // audit log: [0] = count, then 16 floats per entry
 };
 
@@ -2067,6 +2071,8 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), kargs, shmem, c->stream));
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  snprintf(c->last_kernel, sizeof(c->last_kernel), "%s<%d>",
+           (kVariants[var].mask & F_STEP) != 0 ? "render_step_kernel" : "render_kernel", kVariants[var].mask);
   unsigned long long host_cnt[8];
   HIPCHK(c, hipMemcpyAsync(host_cnt, c->work, sizeof(host_cnt), hipMemcpyDeviceToHost, c->stream));
   std::vector<unsigned long long> cost((size_t)a->height);
@@ -2119,6 +2125,7 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
 }
 
 float rt_last_render_ms(const rt_ctx* c) { return c ? c->last_ms : 0.0f; }
+const char* rt_last_render_kernel(const rt_ctx* c) { return c ? c->last_kernel : ""; }
 
 int rt_read_states(rt_ctx* c, int64_t first, int64_t count, uint32_t* out) {
   if (!c || !out || first < 0 || count < 0) return fail(c, RT_ERR_ARG, "bad read_states args");

@@ -18,7 +18,7 @@ run() {  # name timeout cmd...
 STEPS=${STEPS:-tests smoke bench prof}
 for s in $STEPS; do
   case $s in
-    tests) run tests 600 python -m pytest tests -m gpu -x -q ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 3 --warmup 1 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;

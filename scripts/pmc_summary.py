@@ -15,11 +15,11 @@ import sys
 from collections import defaultdict
 
 out = sys.argv[1]
-kname = sys.argv[2] if len(sys.argv) > 2 else "render_kernel"
+kname = sys.argv[2] if len(sys.argv) > 2 else "render_step_kernel<"
 workload = sys.argv[3] if len(sys.argv) > 3 else ""
 
 res = {"kernel": kname, "workload": workload, "dispatches": {}}
-for p in ("prof_fetch", "prof_write", "prof_sq", "prof_sq2"):
+for p in ("prof_fetch", "prof_write", "prof_sq", "prof_sq2", "prof_sq3"):
     per = defaultdict(lambda: defaultdict(float))
     for f in glob.glob(f"gpurun_out/{p}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
