@@ -16,6 +16,7 @@ if the library is missing or the device call fails, the call raises.
 from __future__ import annotations
 
 import ctypes
+import sys
 import os
 from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_uint8, c_uint64, c_void_p
 from dataclasses import dataclass
@@ -288,13 +289,22 @@ class Context:
         self._check(lib().rt_read_states(self._c, first, count, out.ctypes.data), "rt_read_states")
         return out
 
+    def _after_torch(self) -> None:
+        """The C ABI runs on the context's own HIP stream and expects device buffers that are ready:
+        wait for work torch has queued on its current stream (e.g. the fill of a torch.zeros output)."""
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_initialized():
+            torch.cuda.current_stream(self.device).synchronize()
+
     def render(self, args: rt_render_args, fb_dev_ptr: int) -> dict:
+        self._after_torch()
         cnt = rt_counters()
         self._check(lib().rt_render(self._c, ctypes.byref(args), c_void_p(fb_dev_ptr), ctypes.byref(cnt)),
                     "rt_render")
         return cnt.as_dict()
 
     def resolve(self, args: rt_render_args, fb_dev_ptr: int, out_dev_ptr: int) -> None:
+        self._after_torch()
         self._check(lib().rt_resolve(self._c, ctypes.byref(args), c_void_p(fb_dev_ptr), c_void_p(out_dev_ptr)),
                     "rt_resolve")
 

@@ -401,6 +401,50 @@ __device__ __forceinline__ bool prim_t(const DScene& S, int pi, const Ray& r, fl
   return prim_t_q<F>(S, load_prim<F>(S, pi), r, tmin, tmax, t, nprim);
 }
 
+// Candidate range of primitive q for the culled BVH search: an interval [lo, hi] that contains the
+// t the reference's hit() returns, or false when the reference certainly rejects the primitive.
+// Spheres: the discriminant is the reference's own float value (same operations, so the miss
+// test disc < 0 is exact), the root comes from the hardware sqrt and reciprocal (a few ulp)
+// instead of the correctly rounded sqrt and divide; e bounds |root - reference root| with a
+// margin of ~4x (each of sqrt, reciprocal, subtraction and product is within 2 ulp of exact, the
+// reference's own roundings within 0.5 ulp).  The exact root of the winner is computed once, in
+// bvh_settle.  rcpa = rcp(|d|^2) of the query.  Other primitives: their exact t (lo = hi).
+template <int F>
+__device__ __forceinline__ bool prim_range(const DScene& S, const PrimRec& q, const Ray& r, float a, float rcpa,
+                                           float tmin, float tmax, float& lo, float& hi, unsigned& nprim) {
+  const int type = prim_type(q);
+  if (type <= RT_PRIM_MOVING_SPHERE) {
+    if constexpr ((F & F_STATS) != 0) ++nprim;
+    V c = mk(q.a.x, q.a.y, q.a.z);
+    if constexpr ((F & F_MOVING) != 0)
+      if (type == RT_PRIM_MOVING_SPHERE) c = moving_center(q, r.tm);
+    const float rad = q.a.w;
+    const V oc = r.o - c;
+    const float hb = dot(oc, r.d);
+    const float cc = len2(oc) - rad * rad;
+    const float disc = hb * hb - a * cc;
+    if (disc < 0) return false;
+    const float sq = __builtin_amdgcn_sqrtf(disc);
+    const float num = -hb - sq;
+    const float ra = num * rcpa;
+    const float e = __builtin_fmaf((sq + __builtin_fabsf(num)) * 0x1p-19f + 1e-12f, rcpa,
+                                   __builtin_fabsf(ra) * 0x1p-20f);
+    lo = ra - e;
+    hi = ra + e;
+    if (!(e < __builtin_inff())) {  // degenerate direction: no usable bound, the query goes exact
+      lo = -__builtin_inff();
+      hi = __builtin_inff();
+      return true;
+    }
+    return !(hi < tmin || lo > tmax);
+  }
+  float t;
+  if (!prim_t_q<F>(S, q, r, tmin, tmax, t, nprim)) return false;
+  lo = t;
+  hi = t;
+  return true;
+}
+
 // Full hit record of primitive pi at parameter t (the fields hit() sets on success).
 template <int F>
 __device__ void finalize(const DScene& S, int pi, const Ray& r, float tmin, float t, Hit& h) {
@@ -563,18 +607,25 @@ __device__ bool bvh_exact(const DScene& S, int base, int rows, const Ray& r, V i
 // One step of the candidate search of bvh_closest: the node pair of `cur` (one 64-byte record),
 // its primitive children tested right away (leaves hold one primitive), then descend to the nearer
 // hit child (the farther one pushed on the lane's LDS stack) or pop.  Returns false once the
-// search has ended.
+// search has ended.  Candidates are ranges (prim_range): the lane keeps the one with the smallest
+// lo as the winner [blo, bhi] and the smallest lo of every other candidate in `second`; the
+// winner is certain when second > bhi (checked in bvh_settle).  Two exact candidates (lo = hi)
+// compare exactly, as bvh.h does (strictly smaller t, ties to the lower leaf rank), and the
+// loser is not kept in `second`: an exact loser of an exact winner has t >= the winner's t, so
+// when a range later displaces that winner, the winner's lo (added to `second`) covers it.
 template <int F>
-__device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r, V oi, V finv, float tmin, float tmax,
-                                          int& cur, int& sp, float& best, int& best_prim, int& best_rank,
-                                          bool& overflow, unsigned& nnode, unsigned& nprim) {
+__device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r, V oi, V finv, float a, float rcpa,
+                                          float tmin, float tmax, int& cur, int& sp, float& blo, float& bhi,
+                                          float& second, int& best_prim, int& best_rank, bool& overflow,
+                                          unsigned& nnode, unsigned& nprim) {
   stack_t<F>* stk = stack_of<F>(S);
   constexpr int BS = render_block<F>();
   RT_STAMP(3);
   const float4* n = nodes_of<F>(S) + 2 * (fb + 2 * cur);
   const float4 l0 = n[0], l1 = n[1], r0 = n[2], r1 = n[3];
   if constexpr ((F & F_STATS) != 0) nnode += 2;
-  const float cut = __builtin_fminf(best * 1.00390625f, tmax);
+  // bhi >= the winner's exact t: a box entered beyond bhi*(1+2^-8) holds no primitive that can win
+  const float cut = __builtin_fminf(bhi * 1.00390625f, tmax);
   float tl, tr;
   bool hl = fbox(l0, l1, oi, finv, tmin, cut, tl);
   bool hr = fbox(r0, r1, oi, finv, tmin, cut, tr);
@@ -587,13 +638,24 @@ __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r,
       RT_STAMP(4);
       const int pi = -ch - 1;
       const PrimRec q = load_prim<F>(S, pi);
-      float t;
-      if (prim_t_q<F>(S, q, r, tmin, tmax, t, nprim)) {
+      float lo, hi;
+      if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim)) {
         const int rk = __float_as_int(q.c.y);
-        if (t < best || (t == best && rk < best_rank)) {
-          best = t;
+        if (lo == hi && blo == bhi) {  // both exact: the reference's rule, ties to the lower rank
+          if (lo < blo || (lo == blo && rk < best_rank)) {
+            blo = lo;
+            bhi = hi;
+            best_prim = pi;
+            best_rank = rk;
+          }
+        } else if (lo < blo) {
+          second = __builtin_fminf(second, blo);
+          blo = lo;
+          bhi = hi;
           best_prim = pi;
           best_rank = rk;
+        } else {
+          second = __builtin_fminf(second, lo);
         }
       }
       if (side == 0) hl = false; else hr = false;
@@ -620,11 +682,23 @@ __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r,
 // and the reference-chain validation of the candidate (best_rank = its reference leaf rank).
 template <int F>
 __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, const Ray& r, float tmin, float tmax,
-                                           bool overflow, float& best, int& best_prim, int best_rank, unsigned& nnode,
-                                           unsigned& nprim, unsigned& nfall) {
+                                           bool overflow, float bhi, float second, float& best, int& best_prim,
+                                           int best_rank, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   const int last0 = (1 << (rows - 1)) - 1;
   const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-  if (overflow) {  // a subtree was dropped: answer on the exact visit set instead
+  // The candidate search keeps ranges: its winner is certain when every other candidate's range
+  // lies above the winner's (second > bhi), and its exact t (the reference's hit() value) must
+  // pass [tmin, tmax].  Otherwise -- a subtree dropped on stack overflow, overlapping ranges (near
+  // ties), a range straddling tmin -- the query is answered on the exact visit set.
+  // On entry best = the winner's lo (= its exact t when lo = hi).
+  bool sure = !overflow && (best_prim < 0 || second > bhi);  // no candidate at all: a certain miss
+  if (sure && best_prim >= 0 && best != bhi) {
+    float t;
+    unsigned np = 0;
+    sure = prim_t<F>(S, best_prim, r, tmin, tmax, t, np);
+    best = t;
+  }
+  if (!sure) {
     if constexpr ((F & F_STATS) != 0) ++nfall;
     return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
   }
@@ -715,18 +789,22 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
                       __builtin_fminf(__builtin_fmaxf(inv.y, -1e30f), 1e30f),
                       __builtin_fminf(__builtin_fmaxf(inv.z, -1e30f), 1e30f));
     const V oi = mk(r.o.x * finv.x, r.o.y * finv.y, r.o.z * finv.z);
-    best = __builtin_inff();
+    const float a = len2(r.d), rcpa = __builtin_amdgcn_rcpf(a);
+    float blo = __builtin_inff(), bhi = __builtin_inff(), second = __builtin_inff();
     best_prim = -1;
     int best_rank = 0x7fffffff;
     int sp = 0, cur = 0;
     bool overflow = false;
     for (;;) {
       RT_DIAG(0);
-      if (!trav_step<F>(S, fb, r, oi, finv, tmin, tmax, cur, sp, best, best_prim, best_rank, overflow, nnode, nprim))
+      if (!trav_step<F>(S, fb, r, oi, finv, a, rcpa, tmin, tmax, cur, sp, blo, bhi, second, best_prim, best_rank,
+                        overflow, nnode, nprim))
         break;
     }
     RT_STAMP(5);
-    return bvh_settle<F>(S, base, rows, r, tmin, tmax, overflow, best, best_prim, best_rank, nnode, nprim, nfall);
+    best = blo;
+    return bvh_settle<F>(S, base, rows, r, tmin, tmax, overflow, bhi, second, best, best_prim, best_rank, nnode, nprim,
+                         nfall);
   }
 }
 
@@ -1234,6 +1312,11 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
 #ifdef RT_STEP_DIAG
   if (lane < 4) rt_diag_acc[threadIdx.x >> 6][lane] = 0;
 #endif
+#ifdef RT_STAMPS
+  if (lane < kStampPhases + 2) rt_stamp_acc[threadIdx.x >> 6][lane] = 0;
+  __syncthreads();
+  RT_STAMP(0);
+#endif
   const rt_object obj = S.objects[S.world[0]];
   const int tbase = obj.c;  // traversal tree of the world's BVH
   const float tmin = 0.001f, tmax = __builtin_inff();  // render.h:63
@@ -1246,7 +1329,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
   V att = mk(1, 1, 1), col = mk(0, 0, 0);
   V finv = mk(0, 0, 0), oi = mk(0, 0, 0);
   int cur = 0, sp = 0, best_prim = -1, best_rank = 0x7fffffff;
-  float best = 0.0f;
+  float best = 0.0f, bhi = 0.0f, second = 0.0f, qa = 0.0f, rcpa = 0.0f;
   bool overflow = false;
   unsigned nseg = 0, nsamp = 0, item_segs = 0;
   unsigned nnode = 0, nprim = 0, nfall = 0;
@@ -1259,13 +1342,15 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
     {
       RT_DIAG(2);
       // ---- shading phase: finish the ended queries (render.h:60-77)
+      RT_STAMP(7);  // back-to-back pair: phase 7 = the cost of one stamp per loop trip
+      RT_STAMP(5);
       if (mode == 2) {
         ++nseg;
         ++item_segs;
         bool ended = false;
         V contrib;
-        if (!bvh_settle<F>(S, obj.a, obj.b, ray, tmin, tmax, overflow, best, best_prim, best_rank, nnode, nprim,
-                           nfall)) {
+        if (!bvh_settle<F>(S, obj.a, obj.b, ray, tmin, tmax, overflow, bhi, second, best, best_prim, best_rank, nnode,
+                           nprim, nfall)) {
           contrib = att * ld3(S.bg);
           ended = true;
         } else {
@@ -1273,6 +1358,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
           finalize<F>(S, best_prim, ray, tmin, best, h);
           V a, em;
           Ray sc;
+          RT_STAMP(6);
           if (scatter<F>(S, ray, h, a, sc, em, loc)) {
             att = att * a;
             ray = sc;
@@ -1285,6 +1371,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
             ended = true;
           }
         }
+        RT_STAMP(0);
         if (ended) {
           col = col + contrib;
           depth = 0;
@@ -1301,6 +1388,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
         }
         mode = 0;
       }
+      RT_STAMP(0);
       // ---- refill lanes without an item from the wave's chunk of the work counter (one atomic
       // per kChunk items: a single counter serialises its atomics in L2)
       const unsigned long long idle = __ballot(item < 0 && !done);
@@ -1331,6 +1419,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
         }
       }
       // ---- next query: camera ray at a sample's start (render.h:105-108, camera.h:49-58)
+      RT_STAMP(1);
       if (item >= 0 && mode == 0) {
         if (depth == 0) {
           if (s == 0) {
@@ -1352,7 +1441,11 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
                   __builtin_fminf(__builtin_fmaxf(inv.y, -1e30f), 1e30f),
                   __builtin_fminf(__builtin_fmaxf(inv.z, -1e30f), 1e30f));
         oi = mk(ray.o.x * finv.x, ray.o.y * finv.y, ray.o.z * finv.z);
+        qa = len2(ray.d);
+        rcpa = __builtin_amdgcn_rcpf(qa);
         best = __builtin_inff();
+        bhi = __builtin_inff();
+        second = __builtin_inff();
         best_prim = -1;
         best_rank = 0x7fffffff;
         cur = 0;
@@ -1361,14 +1454,15 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
         mode = 1;
       }
     }
+    RT_STAMP(3);
     if (__ballot(mode == 1) == 0) break;  // no item left for any lane of the wave
     // ---- traversal steps until shade_min lanes wait (or none traverses)
     for (;;) {
       RT_DIAG(3);
       if (mode == 1) {
         RT_DIAG(0);
-        if (!trav_step<F>(S, tbase, ray, oi, finv, tmin, tmax, cur, sp, best, best_prim, best_rank, overflow, nnode,
-                          nprim))
+        if (!trav_step<F>(S, tbase, ray, oi, finv, qa, rcpa, tmin, tmax, cur, sp, best, bhi, second, best_prim,
+                          best_rank, overflow, nnode, nprim))
           mode = 2;
       }
       if (__ballot(mode == 1) == 0 || __popcll(__ballot(mode == 2)) >= P.shade_min) break;
@@ -1377,6 +1471,10 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
 
 #ifdef RT_STEP_DIAG
   if (lane < 4) atomicAdd(&rt_diag[lane], rt_diag_acc[threadIdx.x >> 6][lane]);
+#endif
+#ifdef RT_STAMPS
+  RT_STAMP(0);
+  if (lane < kStampPhases) atomicAdd(P.stamps + lane, rt_stamp_acc[threadIdx.x >> 6][2 + lane]);
 #endif
   const unsigned long long ws = wave_sum(nseg), wm = wave_sum(nsamp);
   unsigned long long wn = 0, wp = 0, wf = 0;

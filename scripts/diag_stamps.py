@@ -8,7 +8,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 import raytracing_gpu_amd as rt
 
-PH = ["head/refill", "camera", "world glue", "node tests", "prim tests", "validation+finalize", "scatter", "one stamp (x trips)"]
+PH = ["head/refill (step: sample end + refill)", "camera (step: camera + query setup)", "world glue", "node tests", "prim tests", "validation+finalize", "scatter", "one stamp (x trips)"]
 scene = sys.argv[1]; W, H, spp, nfb = [int(x) for x in sys.argv[2:6]]
 out = "/tmp/stamps.bin"
 if os.path.exists(out):
