@@ -172,6 +172,8 @@ enum rt_cam_mode {
                                      the scene instead of the narrowest (same pixels)           */
 #define RT_FLAG_NO_STEP 16        /* testing: world = one BVH still runs the segment-per-trip
                                      kernel instead of the stepwise one (same pixels)           */
+#define RT_FLAG_NO_SCHEDULE 32    /* natural item order on every launch (no longest-first
+                                     schedule from the previous launch; same pixels)            */
 
 typedef struct rt_render_args {
   int32_t width, height;  /* full image size; N = width*height drives the RNG slots (H3)  */

@@ -1078,6 +1078,13 @@ struct RenderParams {
   int W, H, rows, spp, fb_first, max_depth, cam_mode, fb_count;
   int shade_min;  // render_step_kernel: lanes waiting before a wave runs its shading phase
   int pad4;
+  // Item schedule (see rt_render): perm maps the claimed position to the item (null: identity);
+  // positions below n_long hold the longest items of the previous launch, longest first, and the
+  // waves holding one run at raised priority.  item_cost (measuring launch) receives each item's
+  // segment count.
+  const uint32_t* perm;
+  uint16_t* item_cost;
+  unsigned long long n_long;
   uint32_t cam_state[6];
 #ifdef RT_TRACE
   float* trace;
@@ -1166,7 +1173,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
         if (mine >= P.total_items) {
           done = true;
         } else {
-          item = (long long)mine;
+          item = P.perm ? (long long)P.perm[mine] : (long long)mine;
           // Row-major, fb inside the row, rows in row_order: the costliest rows of the previous
           // launch of this configuration first (else bottom to top), so a launch does not end
           // with a long item started late (a lane runs an item's samples serially).
@@ -1264,6 +1271,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
           dst[1] = out.y;
           dst[2] = out.z;
           if (P.row_cost && (i & 15) == 0) atomicAdd(&P.row_cost[j], (unsigned long long)item_segs);  // a sample ranks rows
+          if (P.item_cost) P.item_cost[item] = (uint16_t)(item_segs < 65535u ? item_segs : 65535u);
           item = -1;
         }
       }
@@ -1337,6 +1345,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
   const rt_camera& C = S.cam;
   unsigned long long chunk_base = 0;  // wave-uniform: next unclaimed item of the wave's chunk
   unsigned chunk_left = 0;
+  bool lng = false;  // the lane's item is one of the longest of the previous launch (perm prefix)
 
   for (;;) {
     {
@@ -1383,6 +1392,7 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
             dst[1] = out.y;
             dst[2] = out.z;
             if (P.row_cost && (i & 15) == 0) atomicAdd(&P.row_cost[j], (unsigned long long)item_segs);
+            if (P.item_cost) P.item_cost[item] = (uint16_t)(item_segs < 65535u ? item_segs : 65535u);
             item = -1;
           }
         }
@@ -1398,7 +1408,8 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
           if (mine >= P.total_items) {
             done = true;
           } else {
-            item = (long long)mine;
+            item = P.perm ? (long long)P.perm[mine] : (long long)mine;
+            lng = mine < P.n_long;
             const long long per_row = (long long)P.fb_count * P.W;  // same item order as render_kernel
             const int q = (int)(item / per_row);
             const long long rem = item - (long long)q * per_row;
@@ -1417,6 +1428,12 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
             col = mk(0, 0, 0);
           }
         }
+      }
+      // Waves holding one of the longest items (processed first) issue ahead of the others, so the
+      // long items of a small multi-GPU share are not the last to finish.
+      if (P.n_long > 0) {
+        if (__ballot(item >= 0 && lng) != 0) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(0);
       }
       // ---- next query: camera ray at a sample's start (render.h:105-108, camera.h:49-58)
       RT_STAMP(1);
@@ -1574,6 +1591,13 @@ struct rt_ctx {
   // next launch of that configuration (no pixel result depends on the order).
   std::vector<unsigned long long> host_cost;
   long long cost_key[5] = {-1, -1, -1, -1, -1};
+  // Item schedule of the last configuration (scene generation, size, spp, depth, fb range, tiling):
+  // per-item segment counts of its measuring launch -> longest items first (perm).
+  uint16_t* item_cost = nullptr;
+  uint32_t* perm = nullptr;
+  long long item_cap = 0;
+  long long perm_key[10] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+  unsigned long long n_long = 0;
   long long scene_gen = 0;
   int cus = 0, blocks_per_cu[32] = {0};  // per kernel variant (kVariants)
   int features = 0;
@@ -1908,6 +1932,8 @@ int rt_ctx_destroy(rt_ctx* c) {
   if (c->work) (void)hipFree(c->work);
   if (c->row_map) (void)hipFree(c->row_map);
   if (c->row_cost) (void)hipFree(c->row_cost);
+  if (c->item_cost) (void)hipFree(c->item_cost);
+  if (c->perm) (void)hipFree(c->perm);
   if (c->dbg) (void)hipFree(c->dbg);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -2077,7 +2103,29 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   // image): there the launch ends with its last long item; with many items per lane bottom-to-top
   // order (sky last in the reference's scenes) measures faster.
   const long long items = (long long)a->fb_count * rows * a->width;
-  if (have_cost && items < 8LL * c->cus * 1024)
+  // Item schedule: the first launch of a configuration records every item's segment count; later
+  // launches process the longest ~2 % first (descending), then the rest in the natural order, and
+  // waves holding a long item run at raised priority.  A lane runs an item's samples serially, so
+  // an item that starts late under full load (22 us per segment per lane on C2) decides when a
+  // small share (a rank of a multi-GPU run) ends.  Pixel results do not depend on the order.
+  const long long pkey[10] = {c->scene_gen, a->width, a->height, a->spp, a->max_depth,
+                              a->fb_first, a->fb_count, a->band_rows, a->band_first, a->band_stride};
+  const bool sched = items <= (64LL << 20) && (a->flags & RT_FLAG_NO_SCHEDULE) == 0;
+  const bool have_perm = sched && std::equal(pkey, pkey + 10, c->perm_key);
+  if (sched && items > c->item_cap) {
+    if (c->item_cost) HIPCHK(c, hipFree(c->item_cost));
+    if (c->perm) HIPCHK(c, hipFree(c->perm));
+    c->item_cost = nullptr;
+    c->perm = nullptr;
+    c->item_cap = 0;
+    std::fill(c->perm_key, c->perm_key + 10, -1LL);
+    HIPCHK(c, hipMalloc((void**)&c->item_cost, (size_t)items * sizeof(uint16_t)));
+    HIPCHK(c, hipMalloc((void**)&c->perm, (size_t)items * sizeof(uint32_t)));
+    c->item_cap = items;
+  }
+  long long order_cap = 8LL * c->cus * 1024;
+  if (const char* e = getenv("RT_COST_ORDER_ITEMS")) order_cap = atoll(e);  // tuning
+  if (!sched && have_cost && items < order_cap)
     std::stable_sort(rm.begin() + rows, rm.end(), [&](int x, int y) { return c->host_cost[rm[x]] > c->host_cost[rm[y]]; });
   HIPCHK(c, hipMemcpyAsync(c->row_map, rm.data(), 2 * (size_t)rows * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemsetAsync(c->work, 0, 8 * sizeof(unsigned long long), c->stream));
@@ -2117,6 +2165,9 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
                                (a->flags & RT_FLAG_WIDEST) != 0, step);
   // shading phase of render_step_kernel once this many lanes of a wave wait (RT_SHADE_MIN: tuning)
   P.shade_min = kShadeMin;
+  P.perm = have_perm ? c->perm : nullptr;
+  P.n_long = have_perm ? c->n_long : 0;
+  P.item_cost = (sched && !have_perm) ? c->item_cost : nullptr;
   if (const char* e = getenv("RT_SHADE_MIN")) P.shade_min = std::max(1, std::min(64, atoi(e)));
   if (check) {
     if (!c->dbg) {
@@ -2183,6 +2234,34 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   }
   if (!have_cost)
     for (int q = 0; q < rows; ++q) c->host_cost[rm[q]] = cost[rm[q]];
+  if (sched && !have_perm) {  // build the schedule of the next launches of this configuration
+    std::vector<uint16_t> ic((size_t)items);
+    HIPCHK(c, hipMemcpy(ic.data(), c->item_cost, ic.size() * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    std::vector<long long> hist(65536, 0);
+    for (uint16_t v : ic) ++hist[v];
+    double pct = 2.0;
+    if (const char* e = getenv("RT_LONG_PCT")) pct = atof(e);  // tuning
+    const long long want = (long long)((double)items * pct / 100.0);
+    int thr = 65535;  // long items: cost >= thr, about `want` of them
+    for (long long acc = 0; thr > 0 && acc + hist[thr] <= want; --thr) acc += hist[thr];
+    ++thr;
+    std::vector<long long> start(65537, 0);  // counting sort of the long items, longest first
+    long long nl = 0;
+    for (int v = 65535; v >= thr; --v) {
+      start[v] = nl;
+      nl += hist[v];
+    }
+    std::vector<uint32_t> pm((size_t)items);
+    long long rest = nl;
+    for (long long k = 0; k < items; ++k) {
+      const int v = ic[(size_t)k];
+      if (v >= thr) pm[(size_t)start[v]++] = (uint32_t)k;
+      else pm[(size_t)rest++] = (uint32_t)k;
+    }
+    HIPCHK(c, hipMemcpy(c->perm, pm.data(), pm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->n_long = (unsigned long long)nl;
+    std::copy(pkey, pkey + 10, c->perm_key);
+  }
   HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
   if (counters) {
     counters->segments = host_cnt[1];

@@ -1,0 +1,55 @@
+"""Diagnostic: strong-scaling estimate of bench.py's N-GPU step on one GPU.
+
+For N in 1, 2, 4, 8 and every rank r < N, times rank r's step pieces as bench.py runs them
+(render_init, the render of its 4-row bands, resolve) with HIP events; the N-GPU step is bounded
+below by max over ranks (the gather and barrier are not modelled).
+
+usage: diag_scale.py [scene W H spp nfb]
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+import raytracing_gpu_amd as rt
+
+scene, W, H, spp, nfb = (sys.argv[1], *[int(x) for x in sys.argv[2:6]]) if len(sys.argv) > 1 else ("big1", 1200, 800, 10, 10)
+ctx = rt.Context(0)
+ctx.upload(rt.Scene.builtin(scene))
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+
+def timed(fn):
+    torch.cuda.synchronize()
+    ev[0].record()
+    fn()
+    ev[1].record()
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1])
+
+
+t_init = min(timed(lambda: ctx.render_init(W, H, 1984)) for _ in range(3))
+base = None
+for n in (1, 2, 4, 8):
+    worst = 0.0
+    segs = 0
+    for r in range(n):
+        args = rt.make_args(W, H, spp, 0, nfb, 50, 0, band_rows=4, band_first=r, band_stride=n)
+        rows = rt.owned_rows(args)
+        fb = torch.empty(nfb * len(rows) * W * 3, dtype=torch.float32, device="cuda")
+        img = torch.empty(len(rows) * W * 3, dtype=torch.uint8, device="cuda")
+        ms = []
+        for _ in range(3):  # the first launch of a configuration measures the row costs
+            c = ctx.render(args, fb.data_ptr())
+            ms.append(ctx.last_render_ms())
+        t_res = timed(lambda: ctx.resolve(args, fb.data_ptr(), img.data_ptr()))
+        worst = max(worst, min(ms[1:]) + t_res)
+        segs += c["segments"]
+        if os.environ.get("VERBOSE"):
+            print(f"   N={n} rank {r}: {min(ms[1:]):.2f} ms, {c['segments']} segments, "
+                  f"{c['segments'] / min(ms[1:]) / 1e3:.0f} Mrays/s", flush=True)
+    step = worst + t_init
+    base = base or step
+    print(f"N={n}: max rank render+resolve {worst:.2f} ms + init {t_init:.2f} ms = {step:.2f} ms/step, "
+          f"{segs / step / 1e3:.0f} Mrays/s, x{base / step:.2f}", flush=True)

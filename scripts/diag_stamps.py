@@ -13,7 +13,8 @@ scene = sys.argv[1]; W, H, spp, nfb = [int(x) for x in sys.argv[2:6]]
 out = "/tmp/stamps.bin"
 if os.path.exists(out):
     os.remove(out)
-ctx = rt.Context(0); ctx.upload(rt.Scene.builtin(scene)); ctx.render_init(W, H, 1984)
+from bench import scene_assets
+ctx = rt.Context(0); ctx.upload(rt.Scene.builtin(scene, **scene_assets(scene)[0])); ctx.render_init(W, H, 1984)
 fb = torch.zeros(nfb * H * W * 3, dtype=torch.float32, device="cuda")
 os.environ["RT_STAMPS_OUT"] = out
 c = ctx.render(rt.make_args(W, H, spp, 0, nfb, 50, 0, lds="nolds" not in sys.argv), fb.data_ptr())
