@@ -1312,6 +1312,10 @@ __global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderP
 // (bvh_settle, finalize), scatter, sample / item bookkeeping, refill from the work counter,
 // the next camera ray and the next query's setup.  Per lane the sequence of RNG draws and float
 // operations is exactly render_kernel's, so frame buffers are bit-identical.
+#ifdef RT_WAVE_TIMES
+__device__ unsigned long long rt_wave_times[3 * 8192];  // per wave: start, global work exhausted, end (s_memtime)
+__device__ unsigned rt_wave_count;
+#endif
 template <int F>
 __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const RenderParams P) {
   const DScene& S = P.S;
@@ -1346,6 +1350,10 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
   unsigned long long chunk_base = 0;  // wave-uniform: next unclaimed item of the wave's chunk
   unsigned chunk_left = 0;
   bool lng = false;  // the lane's item is one of the longest of the previous launch (perm prefix)
+#ifdef RT_WAVE_TIMES
+  unsigned long long wt0, wt1 = 0;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wt0)::"memory");
+#endif
 
   for (;;) {
     {
@@ -1407,6 +1415,9 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
         if (item < 0 && !done) {
           if (mine >= P.total_items) {
             done = true;
+#ifdef RT_WAVE_TIMES
+            if (wt1 == 0) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wt1)::"memory");
+#endif
           } else {
             item = P.perm ? (long long)P.perm[mine] : (long long)mine;
             lng = mine < P.n_long;
@@ -1492,6 +1503,22 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
 #ifdef RT_STAMPS
   RT_STAMP(0);
   if (lane < kStampPhases) atomicAdd(P.stamps + lane, rt_stamp_acc[threadIdx.x >> 6][2 + lane]);
+#endif
+#ifdef RT_WAVE_TIMES
+  {
+    unsigned long long wt2;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wt2)::"memory");
+    const unsigned long long any1 = __ballot(wt1 != 0);
+    const unsigned long long e1 = any1 ? __shfl(wt1, __ffsll((long long)any1) - 1, 64) : 0ull;
+    if (lane == 0) {
+      const unsigned k = atomicAdd(&rt_wave_count, 1u);
+      if (k < 8192) {
+        rt_wave_times[3 * k] = wt0;
+        rt_wave_times[3 * k + 1] = e1;
+        rt_wave_times[3 * k + 2] = wt2;
+      }
+    }
+  }
 #endif
   const unsigned long long ws = wave_sum(nseg), wm = wave_sum(nsamp);
   unsigned long long wn = 0, wp = 0, wf = 0;
@@ -2104,8 +2131,8 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   // order (sky last in the reference's scenes) measures faster.
   const long long items = (long long)a->fb_count * rows * a->width;
   // Item schedule: the first launch of a configuration records every item's segment count; later
-  // launches process the longest ~2 % first (descending), then the rest in the natural order, and
-  // waves holding a long item run at raised priority.  A lane runs an item's samples serially, so
+  // launches process the items longest first (cost buckets of 8 segments, natural order inside a
+  // bucket), and waves holding one of the top ~2 % run at raised priority.  A lane runs an item's samples serially, so
   // an item that starts late under full load (22 us per segment per lane on C2) decides when a
   // small share (a rank of a multi-GPU run) ends.  Pixel results do not depend on the order.
   const long long pkey[10] = {c->scene_gen, a->width, a->height, a->spp, a->max_depth,
@@ -2216,6 +2243,12 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
     hipMemcpyToSymbol(HIP_SYMBOL(rt_diag), z, sizeof(z));
   }
 #endif
+#ifdef RT_WAVE_TIMES
+  {
+    const unsigned z = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(rt_wave_count), &z, sizeof(z));
+  }
+#endif
   void* kargs[] = {&P};
   HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), kargs, shmem, c->stream));
   HIPCHK(c, hipGetLastError());
@@ -2237,27 +2270,27 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   if (sched && !have_perm) {  // build the schedule of the next launches of this configuration
     std::vector<uint16_t> ic((size_t)items);
     HIPCHK(c, hipMemcpy(ic.data(), c->item_cost, ic.size() * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    // Every item in descending cost buckets of 8 segments, the natural (spatially coherent) order
+    // inside a bucket; the top ~2 % by cost are the "long" prefix whose waves run at raised
+    // priority.  (C2, one GPU as rank 0 of N: N = 8 share 3.89 -> 3.45 ms, N = 1 unchanged.)
+    int shift = 3;
+    if (const char* e = getenv("RT_COST_SHIFT")) shift = std::max(0, std::min(12, atoi(e)));  // tuning
+    for (uint16_t& v : ic) v = (uint16_t)(v >> shift);
     std::vector<long long> hist(65536, 0);
     for (uint16_t v : ic) ++hist[v];
+    std::vector<long long> start(65536, 0);  // counting sort, highest bucket first
+    long long acc = 0;
+    for (int v = 65535; v >= 0; --v) {
+      start[v] = acc;
+      acc += hist[v];
+    }
     double pct = 2.0;
     if (const char* e = getenv("RT_LONG_PCT")) pct = atof(e);  // tuning
     const long long want = (long long)((double)items * pct / 100.0);
-    int thr = 65535;  // long items: cost >= thr, about `want` of them
-    for (long long acc = 0; thr > 0 && acc + hist[thr] <= want; --thr) acc += hist[thr];
-    ++thr;
-    std::vector<long long> start(65537, 0);  // counting sort of the long items, longest first
-    long long nl = 0;
-    for (int v = 65535; v >= thr; --v) {
-      start[v] = nl;
-      nl += hist[v];
-    }
+    long long nl = 0;  // whole buckets from the top while they fit in `want`
+    for (int v = 65535; v >= 0 && nl + hist[v] <= want; --v) nl += hist[v];
     std::vector<uint32_t> pm((size_t)items);
-    long long rest = nl;
-    for (long long k = 0; k < items; ++k) {
-      const int v = ic[(size_t)k];
-      if (v >= thr) pm[(size_t)start[v]++] = (uint32_t)k;
-      else pm[(size_t)rest++] = (uint32_t)k;
-    }
+    for (long long k = 0; k < items; ++k) pm[(size_t)start[ic[(size_t)k]]++] = (uint32_t)k;
     HIPCHK(c, hipMemcpy(c->perm, pm.data(), pm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     c->n_long = (unsigned long long)nl;
     std::copy(pkey, pkey + 10, c->perm_key);
@@ -2270,6 +2303,17 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
     counters->samples = host_cnt[4];
     counters->fallbacks = host_cnt[5];
   }
+#ifdef RT_WAVE_TIMES
+  if (const char* out = getenv("RT_WAVE_TIMES_OUT")) {
+    std::vector<unsigned long long> wt(3 * 8192);
+    unsigned n = 0;
+    (void)hipMemcpyFromSymbol(&n, HIP_SYMBOL(rt_wave_count), sizeof(n));
+    (void)hipMemcpyFromSymbol(wt.data(), HIP_SYMBOL(rt_wave_times), wt.size() * sizeof(unsigned long long));
+    FILE* fo = fopen(out, "wb");
+    fwrite(wt.data(), sizeof(unsigned long long), 3 * (size_t)std::min(n, 8192u), fo);
+    fclose(fo);
+  }
+#endif
 #ifdef RT_STEP_DIAG
   {
     unsigned long long h[4];
