@@ -1540,11 +1540,31 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
 
 // curand_init(seed, slot, 0) for every slot < n (render.h:84-92).  Each lane owns kInitChunk
 // consecutive slots: one seed scramble + subsequence jump A^(first * 2^67) applied digit by digit
-// in base 4 (as skipahead_sequence; the digit position's matrix is wave-uniform, lanes mask the
-// applications), then one mat-vec with A^(2^67) per following slot (state(s+1) = A^(2^67) state(s)).
+// in base 4 (as skipahead_sequence: digit d at position i applies (A^(4^i * 2^67))^d), then one
+// mat-vec with A^(2^67) per following slot (state(s+1) = A^(2^67) state(s)).  Every mat-vec on
+// GF(2)^160 goes through byte tables (rt_ctx::jump_tab, built once per context): the image of the
+// state is the XOR of 20 table rows, one per state byte, instead of 160 masked row XORs.
 constexpr int kInitChunk = 16;
+constexpr int kTabRow = 8;                    // words per table row (5 used, 32-byte aligned)
+constexpr int kTabMat = 20 * 256 * kTabRow;   // words per matrix table
+__device__ __forceinline__ void tab_apply(const uint32_t* __restrict__ t, uint32_t v[5]) {
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
+  #pragma unroll
+  for (int b = 0; b < 20; ++b) {
+    const uint32_t byte = (v[b >> 2] >> (8 * (b & 3))) & 0xffu;
+    const uint4 x = *(const uint4*)(t + (b * 256 + byte) * kTabRow);
+    const uint32_t y = t[(b * 256 + byte) * kTabRow + 4];
+    r0 ^= x.x;
+    r1 ^= x.y;
+    r2 ^= x.z;
+    r3 ^= x.w;
+    r4 ^= y;
+  }
+  v[0] = r0; v[1] = r1; v[2] = r2; v[3] = r3; v[4] = r4;
+}
+// jump_tab: table (d - 1) * 32 + i = (A^(4^i * 2^67))^d, d = 1..3; table 0 is the slot step.
 __global__ __launch_bounds__(kBlock) void init_states_kernel(uint4* states, long long n, uint64_t seed,
-                                                            const uint32_t* __restrict__ seq, int digits) {
+                                                            const uint32_t* __restrict__ jump_tab, int digits) {
   const long long first = ((long long)blockIdx.x * kBlock + threadIdx.x) * kInitChunk;
   if (first >= n) return;
   rtx::State st = rtx::seed_state(seed);
@@ -1552,21 +1572,10 @@ __global__ __launch_bounds__(kBlock) void init_states_kernel(uint4* states, long
   for (int d = 0; d < digits; ++d) {
     const unsigned dig = (unsigned)(x & 3u);
     x >>= 2;
-    const uint32_t* m = seq + 800 * d;
-    for (unsigned t = 0; t < 3; ++t) {
-      if (t < dig) {
-        uint32_t out[5];
-        rtx::mat_apply(m, st.v, out);
-        for (int k = 0; k < 5; ++k) st.v[k] = out[k];
-      }
-    }
+    if (dig != 0) tab_apply(jump_tab + (size_t)((dig - 1) * 32 + d) * kTabMat, st.v);
   }
   for (int c = 0; c < kInitChunk && first + c < n; ++c) {
-    if (c > 0) {
-      uint32_t out[5];
-      rtx::mat_apply(seq, st.v, out);
-      for (int k = 0; k < 5; ++k) st.v[k] = out[k];
-    }
+    if (c > 0) tab_apply(jump_tab, st.v);
     const long long slot = first + c;
     states[2 * slot] = make_uint4(st.d, st.v[0], st.v[1], st.v[2]);
     states[2 * slot + 1] = make_uint4(st.v[3], st.v[4], 0u, 0u);
@@ -1609,6 +1618,7 @@ struct rt_ctx {
   long long states_n = 0;
   uint64_t states_seed = 0;
   uint32_t* seq = nullptr;
+  uint32_t* jump_tab = nullptr;  // byte tables of the subsequence jumps (init_states_kernel)
   unsigned long long* work = nullptr;  // [0] work counter, [1..4] counters
   int32_t* row_map = nullptr;  // [rows] owned row -> image row, then [rows] processing order
   int row_cap = 0;
@@ -1930,6 +1940,25 @@ int rt_ctx_create(int hip_device, rt_ctx** out) {
     rtx::build_sequence_jumps(seq.data());
     chk(hipMalloc((void**)&c->seq, seq.size() * 4), "hipMalloc");
     if (rc == RT_OK) chk(hipMemcpy(c->seq, seq.data(), seq.size() * 4, hipMemcpyHostToDevice), "hipMemcpy");
+    // byte tables of M^d for the 32 digit positions M = seq[i], d = 1..3
+    std::vector<uint32_t> tab((size_t)96 * kTabMat, 0u);
+    std::vector<uint32_t> m2(800), m3(800);
+    for (int i = 0; i < 32 && rc == RT_OK; ++i) {
+      const uint32_t* m1 = seq.data() + 800 * i;
+      for (int col = 0; col < 160; ++col) rtx::mat_apply(m1, m1 + 5 * col, m2.data() + 5 * col);  // M^2
+      for (int col = 0; col < 160; ++col) rtx::mat_apply(m1, m2.data() + 5 * col, m3.data() + 5 * col);  // M^3
+      const uint32_t* ms[3] = {m1, m2.data(), m3.data()};
+      for (int d = 0; d < 3; ++d) {
+        uint32_t* t = tab.data() + (size_t)(d * 32 + i) * kTabMat;
+        for (int b = 0; b < 20; ++b)
+          for (int v = 0; v < 256; ++v)
+            for (int j = 0; j < 8; ++j)
+              if ((v >> j) & 1)
+                for (int k = 0; k < 5; ++k) t[(b * 256 + v) * kTabRow + k] ^= ms[d][5 * (8 * b + j) + k];
+      }
+    }
+    if (rc == RT_OK) chk(hipMalloc((void**)&c->jump_tab, tab.size() * 4), "hipMalloc");
+    if (rc == RT_OK) chk(hipMemcpy(c->jump_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice), "hipMemcpy");
   }
   if (rc == RT_OK) {
     hipDeviceProp_t prop;
@@ -1956,6 +1985,7 @@ int rt_ctx_destroy(rt_ctx* c) {
   free_scene(c);
   if (c->states) (void)hipFree(c->states);
   if (c->seq) (void)hipFree(c->seq);
+  if (c->jump_tab) (void)hipFree(c->jump_tab);
   if (c->work) (void)hipFree(c->work);
   if (c->row_map) (void)hipFree(c->row_map);
   if (c->row_cost) (void)hipFree(c->row_cost);
@@ -2091,7 +2121,7 @@ int rt_render_init(rt_ctx* c, int32_t width, int32_t height, uint64_t seed) {
   const long long lanes = (n + kInitChunk - 1) / kInitChunk;
   const long long blocks = (lanes + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(init_states_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, c->states, n, seed,
-                     (const uint32_t*)c->seq, digits);
+                     (const uint32_t*)c->jump_tab, digits);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->states_seed = seed;
