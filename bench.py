@@ -8,7 +8,7 @@ reference camera-RNG mode.  One step = one draw(): render_init + all 10 fb rende
 quantise/average (resolve) [+ the RCCL gather of the 8-bit rows to rank 0 when N > 1].
 A ray segment = one top-level world query (render.h:63), counted on the device.
 
-N > 1 (one process per GPU, torch.distributed over RCCL): rows are dealt in 8-row bands
+N > 1 (one process per GPU, torch.distributed over RCCL): rows are dealt in 4-row bands
 round-robin over ranks; each rank renders and resolves its rows for every fb; one all-gather of
 the 8-bit rows assembles the image.  Strong scaling (the image is fixed).
 """
@@ -28,7 +28,17 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
 NODE_BYTES = 32         # rt_bvh_node
 PRIM_BYTES = 48         # rt_prim
 ITEM_BYTES = 32 + 12    # per (fb, pixel): RNG state read + fb write
+F_LDS = 1 << 13          # variant feature bit: scene staged in LDS (rt_kernels.hip)
+LDS_PEAK_GBS = 150000.0  # ds_read_b64/b128 with every CU streaming (MI355X_MICROARCH.md, LDS)
 VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 1024 SIMD-32s, 2 cycles each (MI355X_MICROARCH.md)
+
+
+def lds_variant(kernel: str) -> bool:
+    """The kernel name carries the variant's feature mask (rt_last_render_kernel): F_LDS set?"""
+    try:
+        return (int(kernel.rsplit("<", 1)[1].rstrip(">")) & F_LDS) != 0
+    except (IndexError, ValueError):
+        return False
 
 
 def committed_pmc(workload: str):
@@ -217,6 +227,15 @@ def main():
                     "node_tests_per_segment": round(stats["node_tests"] / max(stats["segments"], 1), 3),
                     "prim_tests_per_segment": round(stats["prim_tests"] / max(stats["segments"], 1), 3),
                     "fallbacks": stats["fallbacks"]}
+            if lds_variant(kname[0]):
+                # node / primitive records are read from the LDS copy of the scene, not from HBM: the
+                # memory roof that applies to those bytes is the LDS array's, and the binding roof is
+                # VALU issue + LDS latency (see "valu" and DESIGN.md section 3.1)
+                roof["served_from"] = "LDS"
+                roof["lds"] = {"peak": LDS_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / LDS_PEAK_GBS, 4)}
+                roof["note"] = ("achieved = algorithmic node/primitive/item bytes (SURVEY.md 8d) per launch over the "
+                                "kernel time; above the HBM peak because the scene is staged in LDS once per "
+                                "workgroup; measured HBM traffic is 'traffic'")
             pmc = committed_pmc(workload) if world == 1 else None
             if pmc is not None:
                 src, d = pmc

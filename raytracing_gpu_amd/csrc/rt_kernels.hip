@@ -63,6 +63,7 @@ enum : int {
   F_SPHERES = F_MOVING | F_CHECKER | F_BVH,           // basic, first, big1 (C2), two_spheres
   F_CORNELL = F_RECT | F_LIST | F_XFORM | F_MEDIUM,   // cornell, cornell_smoke (C3)
   F_MESH = F_TRI | F_IMAGE | F_BVH | F_LIST,            // triangle meshes with image textures (C4)
+  F_FINAL = F_ALL & ~F_CHECKER,                         // final (C5): everything but the checker texture
 };
 
 namespace {
@@ -1133,8 +1134,25 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
   return x;
 }
 
+// Minimum waves per SIMD the compiler must fit (VGPR budget 512 / waves) for the variants that
+// traverse from global memory, where latency hiding is the limiter: measured on MI355X (C3
+// 800x800 10x100: F_CORNELL at 135 VGPRs / 3 waves 33.2 ms, capped at 128 / 4 waves 28.6 ms; C5
+// 1280x720 8x8: F_ALL at 201 VGPRs / 2 waves 81.4 ms, at 168 / 3 waves 69.1 ms, at 128 / 4 waves
+// with spills 73.2 ms; F_FINAL (no checker code) at 4 waves 66.7 ms, at 3 waves 69.5 ms; C4 door:
+// F_MESH best uncapped, 166 VGPRs / 3 waves).  LDS variants run
+// 1024-thread workgroups, which already cap them at 128.  RT_WPE_GLOBAL overrides (experiments).
 template <int F>
-__global__ __launch_bounds__(render_block<F>()) void render_kernel(const RenderParams P) {
+constexpr int render_wpe() {
+#ifdef RT_WPE_GLOBAL
+  return (F & F_LDS) != 0 ? 1 : RT_WPE_GLOBAL;
+#else
+  constexpr int feat = F & F_ALL;
+  return (F & F_LDS) != 0 ? 1 : ((feat == F_CORNELL || feat == F_FINAL) ? 4 : (feat == F_ALL ? 3 : 1));
+#endif
+}
+template <int F>
+__global__ __launch_bounds__(render_block<F>()) __attribute__((amdgpu_waves_per_eu(render_wpe<F>())))
+void render_kernel(const RenderParams P) {
   const DScene& S = P.S;
   if constexpr ((F & F_LDS) != 0) stage_lds<F>(S);  // nodes, primitives, margins, materials, textures
   const unsigned lane = __lane_id();
@@ -1674,6 +1692,7 @@ const Variant kVariants[] = {
     RT_VARIANT(F_MESH),
     RT_VARIANT(F_MESH | F_STATS),
     RT_VARIANT(F_MESH | F_EXACT),
+    RT_VARIANT(F_FINAL),
 };
 #undef RT_VARIANT
 #undef RT_VARIANT_STEP

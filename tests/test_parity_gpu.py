@@ -260,6 +260,32 @@ def test_culled_equals_exact_full_workload(rtlib, gpu_ctx, scene, W, H, spp, nfb
     assert np.array_equal(_bits(fast), _bits(ex))
 
 
+@pytest.mark.parametrize("scene,W,H,spp,nfb", [
+    ("final", 640, 360, 4, 2),            # C5 composition: ground boxes, xformed BVHs, media, door mesh
+    ("door", 480, 270, 4, 2),             # C4 geometry (the real door mesh)
+])
+def test_culled_equals_exact_asset_scenes(rtlib, gpu_ctx, scene, W, H, spp, nfb):
+    """Mesh / texture scenes at sizes past the oracle's reach: culled traversal (candidate ranges,
+    the sphere validation shortcut) equals the reference visit set, every float."""
+    import os
+
+    import torch
+    from raytracing_gpu_amd import assets
+
+    m = assets.door_mesh_from_fixture(os.path.join(os.path.dirname(__file__), "golden", "door_assimp.npz"))
+    img = assets.synthetic_image(341, 152) if scene == "final" else assets.synthetic_image(1024, 1024)
+    gpu_ctx.upload(rtlib.Scene.builtin(scene, images=[img], meshes=[m]))
+    gpu_ctx.render_init(W, H, 1984)
+    out = []
+    for exact in (False, True):
+        fb = torch.zeros(nfb * H * W * 3, dtype=torch.float32, device="cuda")
+        cnt = gpu_ctx.render(rtlib.make_args(W, H, spp, 0, nfb, 50, REF, exact=exact), fb.data_ptr())
+        out.append((fb.cpu().numpy(), cnt["segments"]))
+    assert out[0][1] == out[1][1]
+    diff = _bits(out[0][0]) != _bits(out[1][0])
+    assert not diff.any(), f"{scene}: {int(diff.sum())} floats differ"
+
+
 @pytest.mark.parametrize("scene,W,H,spp,nfb,cam", [
     ("big1", 1200, 800, 10, 10, REF),     # the whole C2 bench workload
     ("big1", 333, 187, 3, 2, PIX),
