@@ -1511,7 +1511,12 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
                           best_rank, overflow, nnode, nprim))
           mode = 2;
       }
+#ifdef RT_SHADE_MIN_ARG
       if (__ballot(mode == 1) == 0 || __popcll(__ballot(mode == 2)) >= P.shade_min) break;
+#else
+      // compile-time threshold: a kernel-argument operand is re-read by s_load every trip
+      if (__ballot(mode == 1) == 0 || __popcll(__ballot(mode == 2)) >= kShadeMin) break;
+#endif
     }
   }
 
@@ -2239,7 +2244,8 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   const bool step = c->world_bvh && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
   const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
                                (a->flags & RT_FLAG_WIDEST) != 0, step);
-  // shading phase of render_step_kernel once this many lanes of a wave wait (RT_SHADE_MIN: tuning)
+  // shading phase of render_step_kernel once this many lanes of a wave wait (the kernel uses the
+  // constant kShadeMin; RT_SHADE_MIN takes effect in -DRT_SHADE_MIN_ARG builds: tuning)
   P.shade_min = kShadeMin;
   P.perm = have_perm ? c->perm : nullptr;
   P.n_long = have_perm ? c->n_long : 0;
@@ -2319,6 +2325,12 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   if (sched && !have_perm) {  // build the schedule of the next launches of this configuration
     std::vector<uint16_t> ic((size_t)items);
     HIPCHK(c, hipMemcpy(ic.data(), c->item_cost, ic.size() * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    if (const char* e = getenv("RT_ITEM_COST_OUT")) {  // diagnostic: per-item segment counts
+      if (FILE* fo = fopen(e, "wb")) {
+        fwrite(ic.data(), sizeof(uint16_t), ic.size(), fo);
+        fclose(fo);
+      }
+    }
     // Every item in descending cost buckets of 8 segments, the natural (spatially coherent) order
     // inside a bucket; the top ~2 % by cost are the "long" prefix whose waves run at raised
     // priority.  (C2, one GPU as rank 0 of N: N = 8 share 3.89 -> 3.45 ms, N = 1 unchanged.)
