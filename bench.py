@@ -59,8 +59,8 @@ def committed_pmc(workload: str):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scene", default="big1")
     ap.add_argument("--width", type=int, default=1200)
     ap.add_argument("--height", type=int, default=800)
