@@ -914,20 +914,107 @@ __device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, fl
   return true;
 }
 
+// hittable::hit of one top-level object, split in two: object_query finds the hit's t and its
+// primitive (-1: a medium's volume hit) and makes the RNG draws; object_record builds the hit
+// record from them.  world_hit builds only the winning entry's record: the reference copies every
+// closer entry's record (hittable_list.h:23-39), but only the last copy survives and a record is
+// a pure function of (object, primitive, ray, t), so the result is the same bit for bit.
+template <int F>
+__device__ bool object_query(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t, int& prim,
+                             Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+  const rt_object o = S.objects[oi];
+  if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {  // translate(rotate_y(child)), hittable.h:37-59, 112-143
+      Ray moved;
+      const Ray rr = xform_ray(o, r, moved);
+      return leaf_closest<F>(S, S.objects[o.a], rr, tmin, tmax, t, prim, nnode, nprim, nfall);
+  }
+  if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {  // constant_medium.h:34-70 (one RNG draw per qualifying query, H8)
+      const float inf = __builtin_inff();
+      float t1, t2;
+      if (!xform_closest_t<F>(S, o.a, r, -inf, inf, t1, nnode, nprim, nfall)) return false;
+      if (!xform_closest_t<F>(S, o.a, r, t1 + 0.0001f, inf, t2, nnode, nprim, nfall)) return false;
+      if (t1 < tmin) t1 = tmin;
+      if (t2 > tmax) t2 = tmax;
+      if (t1 >= t2) return false;
+      if (t1 < 0) t1 = 0;
+      const float len = __builtin_sqrtf(len2(r.d));
+      const float inside = (t2 - t1) * len;
+      const float hd = o.f[0] * rtm::det_logf(rtx::uniform(rng));
+      if (hd > inside) return false;
+      t = t1 + hd / len;
+      prim = -1;
+      return true;
+  }
+  return leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall);
+}
+
+template <int F>
+__device__ void object_record(const DScene& S, int oi, int prim, const Ray& r, float tmin, float t, Hit& h) {
+  const rt_object o = S.objects[oi];
+  if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {
+      Ray moved;
+      const Ray rr = xform_ray(o, r, moved);
+      finalize<F>(S, prim, rr, tmin, t, h);
+      if (o.b & 2) {
+        const float s = o.f[3], cs = o.f[4];
+        const V p = mk(cs * h.p.x + s * h.p.z, h.p.y, -s * h.p.x + cs * h.p.z);
+        const V n = mk(cs * h.n.x + s * h.n.z, h.n.y, -s * h.n.x + cs * h.n.z);
+        h.p = p;
+        set_face(h, rr, n);  // rotated-frame ray against the world-frame normal (H25)
+      }
+      if (o.b & 1) {
+        h.p = h.p + mk(o.f[0], o.f[1], o.f[2]);
+        set_face(h, moved, h.n);
+      }
+      return;
+  }
+  if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {
+      h.t = t;
+      h.p = r.o + h.t * r.d;
+      h.n = mk(1.0f, 0.0f, 0.0f);
+      h.front = true;
+      h.mat = o.b;
+      h.u = 0.0f;  // stale in the reference; defined as 0
+      h.v = 0.0f;
+      return;
+  }
+  finalize<F>(S, prim, r, tmin, t, h);
+}
+
 // World = hittable_list of top-level objects (render.h:63 with t in [0.001, inf)).
 template <int F>
 __device__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
-  bool any = false;
   float closest = __builtin_inff();
-  for (int w = 0; w < S.n_world; ++w) {
-    Hit tmp;
-    if (object_hit<F>(S, S.world[w], r, 0.001f, closest, tmp, rng, nnode, nprim, nfall)) {
-      any = true;
-      closest = tmp.t;
-      h = tmp;
+  // The widest variants (media and triangles: C5's) keep a record per closer entry: deferring
+  // raises their spills at the 128-VGPR floor (C5 67 -> 85 ms); C3 28.6 -> 21.8 ms with it.
+  constexpr bool defer = (F & (F_MEDIUM | F_TRI)) != (F_MEDIUM | F_TRI);
+  if constexpr (!defer) {
+    bool any = false;
+    for (int w = 0; w < S.n_world; ++w) {
+      Hit tmp;
+      if (object_hit<F>(S, S.world[w], r, 0.001f, closest, tmp, rng, nnode, nprim, nfall)) {
+        any = true;
+        closest = tmp.t;
+        h = tmp;
+      }
     }
+    return any;
+  } else {
+    int wobj = -1, wprim = -1;
+    for (int w = 0; w < S.n_world; ++w) {
+      float t;
+      int pr;
+      const int oi = S.world[w];
+      if (object_query<F>(S, oi, r, 0.001f, closest, t, pr, rng, nnode, nprim, nfall)) {
+        closest = t;
+        wobj = oi;
+        wprim = pr;
+      }
+    }
+    if (wobj < 0) return false;
+    object_record<F>(S, wobj, wprim, r, 0.001f, closest, h);
+    return true;
   }
-  return any;
 }
 
 // ------------------------------------------------------------------ textures (texture.h, perlin.h)
