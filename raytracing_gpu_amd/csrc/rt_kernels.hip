@@ -914,6 +914,55 @@ __device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, fl
   return true;
 }
 
+// Both boundary queries of constant_medium::hit (constant_medium.h:38-44) for a box boundary,
+// optionally under translate/rotate_y, in one pass over the six faces: a face's t and its
+// in-rectangle test do not depend on the query interval, so they are computed once and box.h's
+// list acceptance (tmin <= t <= shrinking t_max, later face wins) is replayed for each interval
+// -- the same float operations on the same operands as the two box_t calls.  Returns 0: the
+// first query missed, 1: the second missed, 2: t1 and t2 set.
+template <int F>
+__device__ int box_boundary_t12(const DScene& S, const rt_object& bo, const PrimRec& q, const Ray& r, float& t1,
+                                float& t2) {
+  Ray moved;
+  const Ray rr = bo.kind == RT_OBJ_XFORM ? xform_ray(bo, r, moved) : r;
+  const V lo = mk(q.a.x, q.a.y, q.a.z), hi = mk(q.a.w, q.b.x, q.b.y);
+  float tt[6];
+  unsigned in = 0;
+#pragma unroll
+  for (int f = 0; f < 6; ++f) {
+    float a0, a1, b0, b1, k;
+    int ax, ia, ib;
+    rect_axes(box_face(lo, hi, f, a0, a1, b0, b1, k), ax, ia, ib);
+    tt[f] = (k - comp(rr.o, ax)) / comp(rr.d, ax);
+    const float a = comp(rr.o, ia) + tt[f] * comp(rr.d, ia);
+    const float b = comp(rr.o, ib) + tt[f] * comp(rr.d, ib);
+    if (!(a < a0 || a > a1 || b < b0 || b > b1)) in |= 1u << f;
+  }
+  const float inf = __builtin_inff();
+  float c = inf;
+  bool h = false;
+#pragma unroll
+  for (int f = 0; f < 6; ++f)
+    if (((in >> f) & 1u) && !(tt[f] < -inf || tt[f] > c)) {
+      c = tt[f];
+      h = true;
+    }
+  if (!h) return 0;
+  t1 = c;
+  const float m = t1 + 0.0001f;
+  c = inf;
+  h = false;
+#pragma unroll
+  for (int f = 0; f < 6; ++f)
+    if (((in >> f) & 1u) && !(tt[f] < m || tt[f] > c)) {
+      c = tt[f];
+      h = true;
+    }
+  if (!h) return 1;
+  t2 = c;
+  return 2;
+}
+
 // hittable::hit of one top-level object, split in two: object_query finds the hit's t and its
 // primitive (-1: a medium's volume hit) and makes the RNG draws; object_record builds the hit
 // record from them.  world_hit builds only the winning entry's record: the reference copies every
@@ -931,8 +980,23 @@ __device__ bool object_query(const DScene& S, int oi, const Ray& r, float tmin, 
   if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {  // constant_medium.h:34-70 (one RNG draw per qualifying query, H8)
       const float inf = __builtin_inff();
       float t1, t2;
-      if (!xform_closest_t<F>(S, o.a, r, -inf, inf, t1, nnode, nprim, nfall)) return false;
-      if (!xform_closest_t<F>(S, o.a, r, t1 + 0.0001f, inf, t2, nnode, nprim, nfall)) return false;
+      bool done = false;
+      if constexpr ((F & F_STATS) == 0 && (F & F_RECT) != 0) {
+        const rt_object bo = S.objects[o.a];
+        const int pi = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].a : bo.a;
+        const bool prim_leaf = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].kind == RT_OBJ_PRIM : bo.kind == RT_OBJ_PRIM;
+        if (prim_leaf) {
+          const PrimRec q = load_prim<F>(S, pi);
+          if (prim_type(q) == RT_PRIM_BOX) {
+            if (box_boundary_t12<F>(S, bo, q, r, t1, t2) < 2) return false;
+            done = true;
+          }
+        }
+      }
+      if (!done) {
+        if (!xform_closest_t<F>(S, o.a, r, -inf, inf, t1, nnode, nprim, nfall)) return false;
+        if (!xform_closest_t<F>(S, o.a, r, t1 + 0.0001f, inf, t2, nnode, nprim, nfall)) return false;
+      }
       if (t1 < tmin) t1 = tmin;
       if (t2 > tmax) t2 = tmax;
       if (t1 >= t2) return false;
