@@ -861,6 +861,18 @@ __device__ bool xform_closest_t(const DScene& S, int oi, const Ray& r, float tmi
   return leaf_closest<F>(S, c, rr, tmin, tmax, t, prim, nnode, nprim, nfall);
 }
 
+// constant_medium::hit over a (moving) sphere boundary after its first boundary query returned
+// t1: sphere.h's second root is its first (H1), so the query from t1 + 1e-4 returns nothing or
+// t1 itself (when t1 + 1e-4 rounds to t1), and with t2 = t1 the clamps to [tmin, tmax] leave
+// t1 >= t2: the medium returns before its RNG draw either way.  A NaN root (degenerate ray) does
+// not, and keeps the reference's path.  Stats variants run the query to count it.
+template <int F>
+__device__ __forceinline__ bool sphere_boundary_no_hit(const DScene& S, int boundary, float t1) {
+  if constexpr ((F & F_STATS) != 0) return false;
+  const rt_object bo = S.objects[boundary];
+  return bo.kind == RT_OBJ_PRIM && t1 == t1 && prim_type(load_prim<F>(S, bo.a)) <= RT_PRIM_MOVING_SPHERE;
+}
+
 // hittable::hit of one top-level object with a complete record.
 template <int F>
 __device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, float tmax, Hit& h, Rng& rng,
@@ -891,6 +903,7 @@ __device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, fl
       const float inf = __builtin_inff();
       float t1, t2;
       if (!xform_closest_t<F>(S, o.a, r, -inf, inf, t1, nnode, nprim, nfall)) return false;
+      if (sphere_boundary_no_hit<F>(S, o.a, t1)) return false;
       if (!xform_closest_t<F>(S, o.a, r, t1 + 0.0001f, inf, t2, nnode, nprim, nfall)) return false;
       if (t1 < tmin) t1 = tmin;
       if (t2 > tmax) t2 = tmax;
