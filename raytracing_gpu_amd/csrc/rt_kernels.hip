@@ -1265,6 +1265,7 @@ constexpr int kAuditCap = 4096;
 constexpr int kRefill = 16;  // refill a wave once this many lanes are idle
 constexpr int kShadeMin = 60;  // render_step_kernel: default shading-phase threshold
 constexpr unsigned kChunk = 64;  // items a wave claims per work-counter atomic
+static_assert(kChunk >= 64, "claim_items: one claim must cover a refill of every lane of a wave");
 
 __device__ __forceinline__ unsigned lane_rank(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
