@@ -2446,8 +2446,8 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
 #ifdef RT_STAMPS
   static unsigned long long* sbuf = nullptr;
-  if (!sbuf) hipMalloc((void**)&sbuf, 8 * sizeof(unsigned long long));
-  hipMemsetAsync(sbuf, 0, 8 * sizeof(unsigned long long), c->stream);
+  if (!sbuf) (void)hipMalloc((void**)&sbuf, 8 * sizeof(unsigned long long));
+  (void)hipMemsetAsync(sbuf, 0, 8 * sizeof(unsigned long long), c->stream);
   P.stamps = sbuf;
 #endif
 #ifdef RT_TRACE
@@ -2551,7 +2551,7 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
 #ifdef RT_STAMPS
   if (getenv("RT_STAMPS_OUT")) {
     unsigned long long hs[8];
-    hipMemcpy(hs, sbuf, sizeof(hs), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(hs, sbuf, sizeof(hs), hipMemcpyDeviceToHost);
     FILE* fo = fopen(getenv("RT_STAMPS_OUT"), "ab");
     fwrite(hs, sizeof(hs), 1, fo);
     fclose(fo);
