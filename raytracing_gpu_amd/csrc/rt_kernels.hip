@@ -1312,7 +1312,7 @@ constexpr int render_wpe() {
   return (F & F_LDS) != 0 ? 1 : RT_WPE_GLOBAL;
 #else
   constexpr int feat = F & F_ALL;
-  return (F & F_LDS) != 0 ? 1 : ((feat == F_CORNELL || feat == F_FINAL) ? 4 : (feat == F_ALL ? 3 : 1));
+  return (F & F_LDS) != 0 ? 1 : ((feat == F_CORNELL || feat == F_FINAL || feat == F_MESH) ? 4 : (feat == F_ALL ? 3 : 1));
 #endif
 }
 template <int F>
