@@ -129,6 +129,12 @@ def test_h9_left_to_right_is_pinned(oracle):
 
 # GPU: full reference width, more samples than the CPU leg (the GPU finishes these in < 1 s each).
 GPU_SPP = {"image11": (10, 100), "image12": (10, 100), "image9": (4, 16)}
+# (min corr, min PSNR dB) at 1200 px: measured on MI355X less a margin.
+GPU_BAR = {
+    "image5.75": (0.999, 41.0), "image6.5": (0.999, 43.0), "image7": (0.993, 32.0), "image8": (0.995, 34.0),
+    "image9": (0.89, 19.0), "image10.75": (0.99, 31.0), "image11": (0.999, 44.0), "image12": (0.998, 33.0),
+    "image13": (0.9999, 56.0), "image14": (0.9999, 50.0), "image15": (0.993, 26.0), "image16": (0.9995, 47.0),
+}
 
 
 @pytest.mark.gpu
@@ -136,7 +142,8 @@ GPU_SPP = {"image11": (10, 100), "image12": (10, 100), "image9": (4, 16)}
 def test_gpu_matches_reference_image(rtlib, gpu_ctx, name):
     d, meta = _fixture()
     scene = meta["images"][name]["scene"]
-    _, _, _, extra, cmin, pmin = CASES[name]
+    extra = CASES[name][3]
+    cmin, pmin = GPU_BAR[name]
     nfb, spp = GPU_SPP.get(name, (4, 8))
     imgs, meshes = scene_assets(scene, d)
     sc = rtlib.Scene.builtin(scene) if imgs is None else rtlib.Scene.builtin(scene, images=imgs, meshes=meshes)
