@@ -29,8 +29,12 @@ NODE_BYTES = 32         # rt_bvh_node
 PRIM_BYTES = 48         # rt_prim
 ITEM_BYTES = 32 + 12    # per (fb, pixel): RNG state read + fb write
 F_LDS = 1 << 13          # variant feature bit: scene staged in LDS (rt_kernels.hip)
-LDS_PEAK_GBS = 150000.0  # ds_read_b64/b128 with every CU streaming (MI355X_MICROARCH.md, LDS)
-VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions/s: 1024 SIMD-32s, 2 cycles each (MI355X_MICROARCH.md)
+# LDS read roof: 256 B/clk/CU for ds_read_b64/b128 (MI355X_MICROARCH.md, LDS [CDNA4]) on
+# 256 CUs at 2.4 GHz = 157.3 TB/s (the guide measures ~150 TB/s with every CU streaming).
+LDS_PEAK_GBS = 256 * 256 * 2.4
+# VALU issue roof: each of the 1024 SIMDs issues one wave64 VALU instruction every 2 cycles
+# (32 lanes/clk: 157.3 TFLOP/s FP32 = 1024 x 32 x 2 x 2.4e9).
+VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2
 
 
 def lds_variant(kernel: str) -> bool:
@@ -41,19 +45,35 @@ def lds_variant(kernel: str) -> bool:
         return False
 
 
-def committed_pmc(workload: str):
-    """PMC summary (scripts/profile.sh + scripts/pmc_summary.py) committed for this exact workload."""
+def committed_pmc(workload: str, kernel: str):
+    """PMC summary (scripts/profile.sh + scripts/pmc_summary.py) committed for this exact workload,
+    kernel instantiation (variant mask included) and device-code build (kernel_build_id: hash of
+    the flags and sources librt_hip.so is built from).  A summary of another build is never used:
+    its counters would describe different code."""
     import glob
 
+    from raytracing_gpu_amd._build import kernel_build_id
+
+    bid = kernel_build_id()
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "*_pmc.json"))):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("workload") == workload and "hbm_bytes_per_launch" in d:
+        if (d.get("workload") == workload and d.get("kernel_full") == kernel and d.get("build_id") == bid
+                and "hbm_bytes_per_launch" in d):
             best = (os.path.relpath(f, ROOT), d)
-    return best
+    return best, bid
+
+
+def cpu_threads() -> tuple[int, int]:
+    """(threads the CPU baseline uses, CPUs this process may run on).  The GPU box gives one GPU's
+    job a 16-CPU share and exports OMP_NUM_THREADS=16 for it while sched_getaffinity still lists
+    the whole machine; the baseline uses the share (the affinity count when no share is set)."""
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(avail, share) if share > 0 else avail), avail
 
 
 def parse():
@@ -106,7 +126,7 @@ def cpu_baseline(a, budget_s: float) -> dict:
     bounded sample of the same workload: every k-th row, all fbs."""
     from oracle import ref_cpu
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, avail = cpu_threads()
     sc = ref_cpu.RefScene(a.scene, **scene_assets(a.scene)[1])
     cam = 0 if a.cam == "ref" else 1
     # calibrate on one row of fb 0
@@ -123,7 +143,16 @@ def cpu_baseline(a, budget_s: float) -> dict:
         segs += c["segments"]
     dt = time.perf_counter() - t0
     rows = len(range(0, a.height, stride))
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {"value": segs / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "host_cpus_visible": avail, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cpu_model": model,
             "sample": f"{a.scene} {a.width}x{a.height}, rows 0::{stride} ({rows} rows) x {a.nfb} fb x {a.spp} spp, "
                       f"{segs} segments in {dt:.1f} s, {threads} threads (oracle/ref_cpu.cpp, g++ -O2)"}
 
@@ -137,6 +166,9 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if a.gpus != world:
+        raise SystemExit(f"bench.py --gpus {a.gpus} but WORLD_SIZE={world}: launch N > 1 with "
+                         f"torch.distributed.run --nproc-per-node {a.gpus}")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.backend == "gloo":  # rehearsal on fewer GPUs than ranks: ranks share devices
         local = local % max(1, torch.cuda.device_count())
@@ -219,36 +251,48 @@ def main():
             items = a.nfb * len(rows) * a.width
             bytes_launch = NODE_BYTES * stats["node_tests"] + PRIM_BYTES * stats["prim_tests"] + ITEM_BYTES * items
             achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
-            roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                    "kernel": kname[0], "kernel_avg_ms": round(avg_ms, 3),
-                    "bytes_per_launch": int(bytes_launch),
-                    "bytes_per_segment": round(bytes_launch / max(stats["segments"], 1), 2),
-                    "node_tests_per_segment": round(stats["node_tests"] / max(stats["segments"], 1), 3),
-                    "prim_tests_per_segment": round(stats["prim_tests"] / max(stats["segments"], 1), 3),
-                    "fallbacks": stats["fallbacks"]}
+            # LDS / memory roof of the algorithmic bytes (node + primitive records + per-item
+            # state and fb bytes).  The LDS variants read node/primitive records from the workgroup's
+            # LDS copy of the scene, the others from L2 / HBM.
+            mem = {"achieved": round(achieved, 2), "unit": "GB/s", "bytes_per_launch": int(bytes_launch),
+                   "bytes_per_segment": round(bytes_launch / max(stats["segments"], 1), 2),
+                   "node_tests_per_segment": round(stats["node_tests"] / max(stats["segments"], 1), 3),
+                   "prim_tests_per_segment": round(stats["prim_tests"] / max(stats["segments"], 1), 3)}
             if lds_variant(kname[0]):
-                # node / primitive records are read from the LDS copy of the scene, not from HBM: the
-                # memory roof that applies to those bytes is the LDS array's, and the binding roof is
-                # VALU issue + LDS latency (see "valu" and DESIGN.md section 3.1)
-                roof["served_from"] = "LDS"
-                roof["lds"] = {"peak": LDS_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / LDS_PEAK_GBS, 4)}
-                roof["note"] = ("achieved = algorithmic node/primitive/item bytes (SURVEY.md 8d) per launch over the "
-                                "kernel time; above the HBM peak because the scene is staged in LDS once per "
-                                "workgroup; measured HBM traffic is 'traffic'")
-            pmc = committed_pmc(workload) if world == 1 else None
+                mem.update(served_from="LDS", peak=round(LDS_PEAK_GBS, 1), frac=round(achieved / LDS_PEAK_GBS, 4))
+            else:
+                mem.update(served_from="L2/HBM", peak=HBM_PEAK_GBS, frac=round(achieved / HBM_PEAK_GBS, 4))
+            roof = {"bound": "lds" if lds_variant(kname[0]) else "hbm", "achieved": mem["achieved"],
+                    "peak": mem["peak"], "unit": "GB/s", "frac": mem["frac"], "traffic": None,
+                    "kernel": kname[0], "kernel_avg_ms": round(avg_ms, 3), "fallbacks": stats["fallbacks"],
+                    "algorithmic": mem}
+            pmc, bid = committed_pmc(workload, kname[0]) if world == 1 else (None, None)
+            roof["build_id"] = bid
             if pmc is not None:
                 src, d = pmc
-                # measured HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE, gfx950 correction)
-                roof["traffic"] = d["hbm_bytes_per_launch"]
-                roof["traffic_source"] = src
+                # Counters are per launch of this same build and workload (rocprofv3 --pmc passes,
+                # scripts/profile.sh); rates use this run's live kernel time.
+                hbm = d["hbm_bytes_per_launch"]  # 2*FETCH_SIZE + WRITE_SIZE (gfx950 correction)
+                roof["traffic"] = hbm
+                roof["hbm"] = {"achieved": round(hbm / (avg_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(hbm / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+                roof["pmc_source"] = src
+                roof["pmc_git_head"] = d.get("git_head")
+                roof["pmc_note"] = "counters committed for this build_id, measured in a separate rocprofv3 run, not this one"
                 if "SQ_INSTS_VALU" in d:
-                    t_issue = d["SQ_INSTS_VALU"] / VALU_ISSUE_PER_S
+                    # binding roof of the megakernel: VALU issue (no MFMA: no dense contraction; the
+                    # scene is LDS/L2-resident, so HBM and the LDS array are far from their roofs)
+                    rate = d["SQ_INSTS_VALU"] / (avg_ms * 1e-3) / 1e9
+                    peak = VALU_ISSUE_PER_S / 1e9
+                    roof.update(bound="valu", achieved=round(rate, 2), peak=round(peak, 1),
+                                unit="G wave64-VALU-inst/s", frac=round(rate / peak, 4))
                     roof["valu"] = {"insts_per_launch": int(d["SQ_INSTS_VALU"]),
-                                    "issue_time_ms": round(t_issue * 1e3, 3),
-                                    "issue_frac": round(t_issue / (avg_ms * 1e-3), 4),
-                                    "lane_utilisation": round(d.get("valu_lane_utilisation", float("nan")), 4),
-                                    "source": src}
+                                    "lane_utilisation": round(d.get("valu_lane_utilisation", float("nan")), 4)}
+                    if "SQ_WAIT_ANY" in d and "SQ_WAVE_CYCLES" in d:
+                        roof["valu"]["wait_any_share"] = round(d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"], 4)
+                    if "SQ_LDS_BANK_CONFLICT" in d and "SQ_LDS_IDX_ACTIVE" in d:
+                        roof["valu"]["lds_bank_conflict_share"] = round(
+                            d["SQ_LDS_BANK_CONFLICT"] / max(d["SQ_LDS_IDX_ACTIVE"], 1), 4)
         out = {
             "metric": "Mrays/sec (primary+bounces) on RTIOW random-spheres 1200x800x100spp",
             "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,

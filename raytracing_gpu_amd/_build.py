@@ -24,6 +24,21 @@ HIPCC_FLAGS = [
 ]
 
 
+def kernel_build_id() -> str:
+    """Identity of the device code: sha256 over the compile flags and every source the library is
+    built from.  PMC summaries record it (scripts/pmc_summary.py) and bench.py uses a summary's
+    counters only when the id matches the library it runs."""
+    import hashlib
+
+    h = hashlib.sha256(" ".join(HIPCC_FLAGS).encode())
+    for f in HIP_DEPS:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    with open(os.path.join(ROOT, "include", "rt_hip.h"), "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def _stale(target: str, deps: list[str]) -> bool:
     if not os.path.exists(target):
         return True

@@ -39,9 +39,9 @@ const uint8_t kDezigzag[64 + 15] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 
 struct Huff {
   // canonical code tables: for each code length L, codes [mincode[L], maxcode[L]] map to
   // values starting at valptr[L]
-  int mincode[17], maxcode[18], valptr[17];
-  uint8_t vals[256];
-  bool present = false;
+  int mincode[17] = {}, maxcode[18] = {}, valptr[17] = {};
+  uint8_t vals[256] = {};
+  bool present = false;  // defined by a DHT segment
 };
 
 struct Comp {
@@ -54,7 +54,7 @@ struct Comp {
 struct Jpeg {
   const uint8_t* p;
   const uint8_t* end;
-  uint16_t dequant[4][64];
+  uint16_t dequant[4][64] = {};
   Huff dc[4], ac[4];
   Comp comp[4];
   int ncomp = 0, width = 0, height = 0, hmax = 1, vmax = 1, restart = 0;
@@ -125,6 +125,9 @@ inline uint8_t clamp255(int x) { return x < 0 ? 0 : (x > 255 ? 255 : (uint8_t)x)
 // 12-bit fixed-point IDCT constants, rounded from float: (int)(c * 4096 + 0.5).
 constexpr int fx(float c) { return (int)((double)(c * 4096.0f) + 0.5); }
 
+// Attribution: idct_1d / idct_block follow stb_image v2.26's stbi__idct_block (Sean Barrett,
+// public domain / MIT; vendored by the reference at external/stb_image.h:2356-2449), itself
+// derived from the IJG's jidctint.c: bit-exact texels need the identical integer arithmetic.
 // One 1-D pass of the jidctint-derived IDCT over s0..s7; outputs the even part x0..x3 and
 // odd part t0..t3 (results are x_k +- t_(3-k)).
 inline void idct_1d(int s0, int s1, int s2, int s3, int s4, int s5, int s6, int s7, int& x0, int& x1, int& x2,
@@ -379,8 +382,14 @@ bool parse(Jpeg& j) {
         int k = 0;
         while (k < j.ncomp && j.comp[k].id != id) ++k;
         if (k == j.ncomp) return (j.err = "bad SOS component", false);
+        // stb_image v2.26 rejects selectors past its 4 tables ('bad DC huff' / 'bad AC huff')
+        if ((tt >> 4) > 3) return (j.err = "bad DC huff", false);
+        if ((tt & 15) > 3) return (j.err = "bad AC huff", false);
         j.comp[k].td = tt >> 4;
         j.comp[k].ta = tt & 15;
+        // a scan may only select tables a DHT segment defined
+        if (!j.dc[j.comp[k].td].present || !j.ac[j.comp[k].ta].present)
+          return (j.err = "scan selects an undefined Huffman table", false);
         scomp[q] = k;
       }
       j.p = seg_end;  // Ss, Se, Ah/Al: sequential baseline ignores them
@@ -474,7 +483,7 @@ extern "C" {
 int rt_image_decode(const uint8_t* bytes, int64_t n, rt_image_host** out) {
   if (!bytes || n <= 0 || !out) return RT_ERR_ARG;
   *out = nullptr;
-  std::unique_ptr<Jpeg> j(new Jpeg);
+  std::unique_ptr<Jpeg> j(new Jpeg());
   j->p = bytes;
   j->end = bytes + n;
   memset(j->dequant, 0, sizeof(j->dequant));

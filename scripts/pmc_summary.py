@@ -11,14 +11,24 @@ Kernel durations come from gpurun_out/prof_trace/**/run_kernel_stats.csv.
 import csv
 import glob
 import json
+import os
+import subprocess
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from raytracing_gpu_amd._build import kernel_build_id  # noqa: E402
 
 out = sys.argv[1]
 kname = sys.argv[2] if len(sys.argv) > 2 else "render_step_kernel<"
 workload = sys.argv[3] if len(sys.argv) > 3 else ""
 
-res = {"kernel": kname, "workload": workload, "dispatches": {}}
+res = {"kernel": kname, "workload": workload, "build_id": kernel_build_id(), "dispatches": {}}
+try:
+    res["git_head"] = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                                     text=True).stdout.strip() or None
+except OSError:
+    res["git_head"] = None
 for p in ("prof_fetch", "prof_write", "prof_sq", "prof_sq2", "prof_sq3"):
     per = defaultdict(lambda: defaultdict(float))
     for f in glob.glob(f"gpurun_out/{p}/**/*counter_collection.csv", recursive=True):
@@ -34,6 +44,10 @@ for f in glob.glob("gpurun_out/prof_trace/**/*kernel_stats.csv", recursive=True)
         if kname in row["Name"]:
             res.setdefault("trace", []).append({"name": row["Name"][:120], "calls": int(row["Calls"]),
                                                 "avg_ms": float(row["AverageNs"]) / 1e6})
+names = {t["name"] for t in res.get("trace", [])}
+if len(names) == 1:  # the full instantiation, e.g. render_step_kernel<25730>: bench.py matches on it
+    n = names.pop()
+    res["kernel_full"] = n.split("::", 1)[-1].split("(", 1)[0]
 if "FETCH_SIZE" in res and "WRITE_SIZE" in res:
     res["hbm_bytes_per_launch"] = int((2 * res["FETCH_SIZE"] + res["WRITE_SIZE"]) * 1024)
     res["hbm_correction"] = "2*FETCH_SIZE + WRITE_SIZE, KiB (MI355X_MICROARCH.md, HBM [CDNA4])"

@@ -53,3 +53,25 @@ def test_rejects_non_jpeg(rtlib):
 
     with pytest.raises(Exception):
         assets.decode_jpeg(b"\x89PNG\r\n\x1a\n" + b"\0" * 64)
+
+
+def _with_sos_selector(data: bytes, tt: int) -> bytes:
+    """The file with the first scan component's Huffman table selector byte replaced."""
+    k = data.index(b"\xff\xda")
+    # FFDA, Ls (2), Ns (1), then (Cs, Td<<4|Ta) pairs
+    b = bytearray(data)
+    b[k + 6] = tt
+    return bytes(b)
+
+
+@pytest.mark.parametrize("tt", [0x50, 0x05, 0xF0, 0x22], ids=["dc5", "ac5", "dc15", "undefined2"])
+def test_rejects_bad_huffman_selectors(rtlib, tt):
+    """SOS table selectors past the 4 tables, or naming a table no DHT defined, are rejected (stb_image
+    v2.26: 'bad DC huff' / 'bad AC huff') instead of indexing out of bounds / uninitialised tables."""
+    from raytracing_gpu_amd import assets
+
+    with open(os.path.join(JPEG, "rgb444.jpg"), "rb") as f:
+        data = f.read()
+    assets.decode_jpeg(_with_sos_selector(data, 0x00))  # table 0/0 is defined: still decodes
+    with pytest.raises(Exception):
+        assets.decode_jpeg(_with_sos_selector(data, tt))
