@@ -13,6 +13,9 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "librt_hip.so")
+MULTI_LIB = os.path.join(PKG, "librt_multi.so")
+EXAMPLES = os.path.join(ROOT, "examples")
+RT_MAIN = os.path.join(EXAMPLES, "bin", "rt_main")
 
 HIP_SOURCES = ["rt_kernels.hip", "rt_scene.cpp", "rt_obj.cpp", "rt_image.cpp"]
 HIP_DEPS = HIP_SOURCES + ["rt_detmath.h", "rt_xorwow.h", "rt_host_geom.h"]
@@ -59,6 +62,40 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+def build_multi(force: bool = False, verbose: bool = False) -> str:
+    """librt_multi.so: the multi-GPU draw() (csrc/rt_multi.cpp, include/rt_multi.h), host C++ over
+    librt_hip.so and RCCL (/opt/rocm/lib/librccl.so)."""
+    deps = [os.path.join(CSRC, "rt_multi.cpp"), os.path.join(ROOT, "include", "rt_multi.h"), LIB]
+    if not force and not _stale(MULTI_LIB, deps):
+        return MULTI_LIB
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, "-O2", "-std=c++17", "-fPIC", "-shared", "-o", MULTI_LIB + ".tmp", os.path.join(CSRC, "rt_multi.cpp"),
+           "-L" + PKG, "-lrt_hip", "-lrccl", "-lpthread", "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(MULTI_LIB + ".tmp", MULTI_LIB)
+    return MULTI_LIB
+
+
+def build_examples(force: bool = False, verbose: bool = False) -> str:
+    """examples/bin/rt_main: the reference's main.cu as a C++ caller of include/rt_hip.h and
+    include/rt_multi.h, linked against the in-tree libraries."""
+    src = os.path.join(EXAMPLES, "rt_main.cpp")
+    deps = [src, os.path.join(ROOT, "include", "rt_hip.h"), os.path.join(ROOT, "include", "rt_multi.h"), LIB, MULTI_LIB]
+    if not force and not _stale(RT_MAIN, deps):
+        return RT_MAIN
+    os.makedirs(os.path.dirname(RT_MAIN), exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, "-O2", "-std=c++17", "-I" + os.path.join(ROOT, "include"), "-o", RT_MAIN + ".tmp", src,
+           "-L" + PKG, "-lrt_hip", "-lrt_multi", "-Wl,-rpath,$ORIGIN/../../raytracing_gpu_amd", "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True, cwd=EXAMPLES)
+    os.replace(RT_MAIN + ".tmp", RT_MAIN)
+    return RT_MAIN
+
+
 def build_oracle(force: bool = False) -> str:
     odir = os.path.join(ROOT, "oracle")
     args = ["make", "-C", odir, "-j4"]
@@ -73,5 +110,7 @@ def build_oracle(force: bool = False) -> str:
 
 if __name__ == "__main__":
     build_hip(force="--force" in sys.argv, verbose=True)
+    build_multi(force="--force" in sys.argv, verbose=True)
+    build_examples(force="--force" in sys.argv, verbose=True)
     build_oracle(force="--force" in sys.argv)
     print(LIB)

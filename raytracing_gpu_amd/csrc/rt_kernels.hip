@@ -2489,7 +2489,8 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
     for (int q = 0; q < rows; ++q) c->host_cost[rm[q]] = cost[rm[q]];
   if (sched && !have_perm) {  // build the schedule of the next launches of this configuration
     std::vector<uint16_t> ic((size_t)items);
-    HIPCHK(c, hipMemcpy(ic.data(), c->item_cost, ic.size() * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpyAsync(ic.data(), c->item_cost, ic.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     if (const char* e = getenv("RT_ITEM_COST_OUT")) {  // diagnostic: per-item segment counts
       if (FILE* fo = fopen(e, "wb")) {
         fwrite(ic.data(), sizeof(uint16_t), ic.size(), fo);
@@ -2517,7 +2518,9 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
     for (int v = 65535; v >= 0 && nl + hist[v] <= want; --v) nl += hist[v];
     std::vector<uint32_t> pm((size_t)items);
     for (long long k = 0; k < items; ++k) pm[(size_t)start[ic[(size_t)k]]++] = (uint32_t)k;
-    HIPCHK(c, hipMemcpy(c->perm, pm.data(), pm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    // on the context's stream, completed before returning: the next launch (same stream) reads it
+    HIPCHK(c, hipMemcpyAsync(c->perm, pm.data(), pm.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     c->n_long = (unsigned long long)nl;
     std::copy(pkey, pkey + 10, c->perm_key);
   }
