@@ -144,6 +144,24 @@ __device__ __forceinline__ stack_t<F>* stack_of(const DScene& S) {
     return (short*)(rt_lds + lds_mats_at(S) + S.lds_mats + 2 * S.lds_texs) + threadIdx.x;
   else return (int*)rt_lds + threadIdx.x;
 }
+// Per-lane traversal stack in LDS (after the staged scene for F_LDS variants), lane-interleaved
+// (entry d of thread t at [d * block + t]) so a wave's pushes/pops hit 64 distinct banks.
+constexpr int kStackDepth = 16;
+// Per-lane "locker" of render_kernel's global-memory variants: cold per-item / per-sample state
+// (the camera RNG copy, the sample sum, the item's fb and row) kept in LDS after the stacks,
+// lane-interleaved (word k of thread t at [k * block + t]), instead of VGPRs: it is touched once
+// per sample, and without it the variants' live state spills to scratch inside the traversal
+// loops (F_FINAL: 744 B per lane, ~340 B of scratch stores per segment, missing L2).
+constexpr int kLocker = 12;
+template <int F>
+constexpr bool parks() {
+  return (F & F_LDS) == 0;
+}
+template <int F>
+__device__ __forceinline__ uint32_t* locker_of() {
+  return (uint32_t*)rt_lds + render_block<F>() * kStackDepth + threadIdx.x;
+}
+
 // Stage the read-only scene arrays a F_LDS variant reads in LDS, once per workgroup.
 template <int F>
 __device__ __forceinline__ void stage_lds(const DScene& S) {
@@ -160,9 +178,6 @@ __device__ __forceinline__ void stage_lds(const DScene& S) {
   __syncthreads();
 }
 
-// Per-lane traversal stack in LDS (after the staged scene for F_LDS variants), lane-interleaved
-// (entry d of thread t at [d * block + t]) so a wave's pushes/pops hit 64 distinct banks.
-constexpr int kStackDepth = 16;
 
 // Diagnostic build only (-DRT_STAMPS): per-wave cycle shares of the render loop's phases
 // (s_memtime stamps, cdna_hip_programming.md section 7).  Phase = code run after the stamp.
@@ -873,60 +888,6 @@ __device__ __forceinline__ bool sphere_boundary_no_hit(const DScene& S, int boun
   return bo.kind == RT_OBJ_PRIM && t1 == t1 && prim_type(load_prim<F>(S, bo.a)) <= RT_PRIM_MOVING_SPHERE;
 }
 
-// hittable::hit of one top-level object with a complete record.
-template <int F>
-__device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, float tmax, Hit& h, Rng& rng,
-                           unsigned& nnode, unsigned& nprim, unsigned& nfall) {
-  const rt_object o = S.objects[oi];
-  float t;
-  int prim;
-  if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {  // translate(rotate_y(child)), hittable.h:37-59, 112-143
-      Ray moved;
-      const Ray rr = xform_ray(o, r, moved);
-      const rt_object c = S.objects[o.a];
-      if (!leaf_closest<F>(S, c, rr, tmin, tmax, t, prim, nnode, nprim, nfall)) return false;
-      finalize<F>(S, prim, rr, tmin, t, h);
-      if (o.b & 2) {
-        const float s = o.f[3], cs = o.f[4];
-        const V p = mk(cs * h.p.x + s * h.p.z, h.p.y, -s * h.p.x + cs * h.p.z);
-        const V n = mk(cs * h.n.x + s * h.n.z, h.n.y, -s * h.n.x + cs * h.n.z);
-        h.p = p;
-        set_face(h, rr, n);  // rotated-frame ray against the world-frame normal (H25)
-      }
-      if (o.b & 1) {
-        h.p = h.p + mk(o.f[0], o.f[1], o.f[2]);
-        set_face(h, moved, h.n);
-      }
-      return true;
-  }
-  if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {  // constant_medium.h:34-70 (one RNG draw per qualifying query, H8)
-      const float inf = __builtin_inff();
-      float t1, t2;
-      if (!xform_closest_t<F>(S, o.a, r, -inf, inf, t1, nnode, nprim, nfall)) return false;
-      if (sphere_boundary_no_hit<F>(S, o.a, t1)) return false;
-      if (!xform_closest_t<F>(S, o.a, r, t1 + 0.0001f, inf, t2, nnode, nprim, nfall)) return false;
-      if (t1 < tmin) t1 = tmin;
-      if (t2 > tmax) t2 = tmax;
-      if (t1 >= t2) return false;
-      if (t1 < 0) t1 = 0;
-      const float len = __builtin_sqrtf(len2(r.d));
-      const float inside = (t2 - t1) * len;
-      const float hd = o.f[0] * rtm::det_logf(rtx::uniform(rng));
-      if (hd > inside) return false;
-      h.t = t1 + hd / len;
-      h.p = r.o + h.t * r.d;
-      h.n = mk(1.0f, 0.0f, 0.0f);
-      h.front = true;
-      h.mat = o.b;
-      h.u = 0.0f;  // stale in the reference; defined as 0
-      h.v = 0.0f;
-      return true;
-  }
-  if (!leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall)) return false;
-  finalize<F>(S, prim, r, tmin, t, h);
-  return true;
-}
-
 // Both boundary queries of constant_medium::hit (constant_medium.h:38-44) for a box boundary,
 // optionally under translate/rotate_y, in one pass over the six faces: a face's t and its
 // in-rectangle test do not depend on the query interval, so they are computed once and box.h's
@@ -976,6 +937,86 @@ __device__ int box_boundary_t12(const DScene& S, const rt_object& bo, const Prim
   return 2;
 }
 
+// The two boundary queries of constant_medium::hit (constant_medium.h:38-44): t1 over (-inf, inf),
+// t2 from t1 + 1e-4.  Returns false when either misses (or, for a sphere boundary, when the second
+// query cannot hit: sphere_boundary_no_hit).  Primitive boundaries are answered inline: the
+// general path (xform_closest_t) stays out of line in the widest variants, and a call spills
+// every live VGPR of the kernel to scratch around it.
+template <int F>
+__device__ __forceinline__ bool medium_boundary(const DScene& S, const rt_object& o, const Ray& r, float& t1, float& t2,
+                                                unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+  const float inf = __builtin_inff();
+  if constexpr ((F & F_STATS) == 0) {  // stats variants run the reference's two queries to count them
+    const rt_object bo = S.objects[o.a];
+    const bool prim_leaf = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].kind == RT_OBJ_PRIM : bo.kind == RT_OBJ_PRIM;
+    if (prim_leaf) {
+      const int pi = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].a : bo.a;
+      const PrimRec q = load_prim<F>(S, pi);
+      if ((F & F_RECT) != 0 && prim_type(q) == RT_PRIM_BOX) return box_boundary_t12<F>(S, bo, q, r, t1, t2) == 2;
+      if (bo.kind == RT_OBJ_PRIM) {
+        unsigned np = 0;
+        if (!prim_t_q<F>(S, q, r, -inf, inf, t1, np)) return false;
+        if (prim_type(q) <= RT_PRIM_MOVING_SPHERE && t1 == t1) return false;  // sphere_boundary_no_hit
+        return prim_t_q<F>(S, q, r, t1 + 0.0001f, inf, t2, np);
+      }
+    }
+  }
+  if (!xform_closest_t<F>(S, o.a, r, -inf, inf, t1, nnode, nprim, nfall)) return false;
+  if (sphere_boundary_no_hit<F>(S, o.a, t1)) return false;
+  return xform_closest_t<F>(S, o.a, r, t1 + 0.0001f, inf, t2, nnode, nprim, nfall);
+}
+
+// hittable::hit of one top-level object with a complete record.
+template <int F>
+__device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, float tmax, Hit& h, Rng& rng,
+                           unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+  const rt_object o = S.objects[oi];
+  float t;
+  int prim;
+  if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {  // translate(rotate_y(child)), hittable.h:37-59, 112-143
+      Ray moved;
+      const Ray rr = xform_ray(o, r, moved);
+      const rt_object c = S.objects[o.a];
+      if (!leaf_closest<F>(S, c, rr, tmin, tmax, t, prim, nnode, nprim, nfall)) return false;
+      finalize<F>(S, prim, rr, tmin, t, h);
+      if (o.b & 2) {
+        const float s = o.f[3], cs = o.f[4];
+        const V p = mk(cs * h.p.x + s * h.p.z, h.p.y, -s * h.p.x + cs * h.p.z);
+        const V n = mk(cs * h.n.x + s * h.n.z, h.n.y, -s * h.n.x + cs * h.n.z);
+        h.p = p;
+        set_face(h, rr, n);  // rotated-frame ray against the world-frame normal (H25)
+      }
+      if (o.b & 1) {
+        h.p = h.p + mk(o.f[0], o.f[1], o.f[2]);
+        set_face(h, moved, h.n);
+      }
+      return true;
+  }
+  if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {  // constant_medium.h:34-70 (one RNG draw per qualifying query, H8)
+      float t1, t2;
+      if (!medium_boundary<F>(S, o, r, t1, t2, nnode, nprim, nfall)) return false;
+      if (t1 < tmin) t1 = tmin;
+      if (t2 > tmax) t2 = tmax;
+      if (t1 >= t2) return false;
+      if (t1 < 0) t1 = 0;
+      const float len = __builtin_sqrtf(len2(r.d));
+      const float inside = (t2 - t1) * len;
+      const float hd = o.f[0] * rtm::det_logf(rtx::uniform(rng));
+      if (hd > inside) return false;
+      h.t = t1 + hd / len;
+      h.p = r.o + h.t * r.d;
+      h.n = mk(1.0f, 0.0f, 0.0f);
+      h.front = true;
+      h.mat = o.b;
+      h.u = 0.0f;  // stale in the reference; defined as 0
+      h.v = 0.0f;
+      return true;
+  }
+  if (!leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall)) return false;
+  finalize<F>(S, prim, r, tmin, t, h);
+  return true;
+}
+
 // hittable::hit of one top-level object, split in two: object_query finds the hit's t and its
 // primitive (-1: a medium's volume hit) and makes the RNG draws; object_record builds the hit
 // record from them.  world_hit builds only the winning entry's record: the reference copies every
@@ -991,25 +1032,8 @@ __device__ bool object_query(const DScene& S, int oi, const Ray& r, float tmin, 
       return leaf_closest<F>(S, S.objects[o.a], rr, tmin, tmax, t, prim, nnode, nprim, nfall);
   }
   if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {  // constant_medium.h:34-70 (one RNG draw per qualifying query, H8)
-      const float inf = __builtin_inff();
       float t1, t2;
-      bool done = false;
-      if constexpr ((F & F_STATS) == 0 && (F & F_RECT) != 0) {
-        const rt_object bo = S.objects[o.a];
-        const int pi = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].a : bo.a;
-        const bool prim_leaf = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].kind == RT_OBJ_PRIM : bo.kind == RT_OBJ_PRIM;
-        if (prim_leaf) {
-          const PrimRec q = load_prim<F>(S, pi);
-          if (prim_type(q) == RT_PRIM_BOX) {
-            if (box_boundary_t12<F>(S, bo, q, r, t1, t2) < 2) return false;
-            done = true;
-          }
-        }
-      }
-      if (!done) {
-        if (!xform_closest_t<F>(S, o.a, r, -inf, inf, t1, nnode, nprim, nfall)) return false;
-        if (!xform_closest_t<F>(S, o.a, r, t1 + 0.0001f, inf, t2, nnode, nprim, nfall)) return false;
-      }
+      if (!medium_boundary<F>(S, o, r, t1, t2, nnode, nprim, nfall)) return false;
       if (t1 < tmin) t1 = tmin;
       if (t2 > tmax) t2 = tmax;
       if (t1 >= t2) return false;
@@ -1064,7 +1088,11 @@ __device__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsig
   float closest = __builtin_inff();
   // The widest variants (media and triangles: C5's) keep a record per closer entry: deferring
   // raises their spills at the 128-VGPR floor (C5 67 -> 85 ms); C3 28.6 -> 21.8 ms with it.
+#ifdef RT_DEFER_ALL
+  constexpr bool defer = true;
+#else
   constexpr bool defer = (F & (F_MEDIUM | F_TRI)) != (F_MEDIUM | F_TRI);
+#endif
   if constexpr (!defer) {
     bool any = false;
     for (int w = 0; w < S.n_world; ++w) {
@@ -1335,13 +1363,16 @@ void render_kernel(const RenderParams P) {
   Rng loc{}, cam{};
   Ray ray{};
   V att = mk(1, 1, 1), col = mk(0, 0, 0);
-  unsigned long long nseg = 0, nsamp = 0;
+  unsigned nseg = 0, nsamp = 0;
   unsigned item_segs = 0;
   unsigned nnode = 0, nprim = 0, nfall = 0;
   const bool per_pixel = P.cam_mode == RT_CAM_PER_PIXEL;
   const rt_camera& C = S.cam;
   unsigned long long chunk_base = 0;  // wave-uniform: next unclaimed item of the wave's chunk
   unsigned chunk_left = 0;
+  // cold state in the LDS locker (parks<F>): 0..5 camera RNG, 6..8 sample sum, 9 fb, 10 owned row
+  uint32_t* const lk = locker_of<F>();
+  constexpr int LB = render_block<F>();
 
   for (;;) {
     // ---- refill idle lanes (one atomic per wave, ballot-compacted ranks)
@@ -1375,7 +1406,15 @@ void render_kernel(const RenderParams P) {
           s = 0;
           depth = 0;
           item_segs = 0;
-          col = mk(0, 0, 0);
+          if constexpr (parks<F>()) {
+            lk[6 * LB] = 0u;
+            lk[7 * LB] = 0u;
+            lk[8 * LB] = 0u;
+            lk[9 * LB] = (uint32_t)f;
+            lk[10 * LB] = (uint32_t)r;
+          } else {
+            col = mk(0, 0, 0);
+          }
         }
       }
     }
@@ -1387,6 +1426,9 @@ void render_kernel(const RenderParams P) {
         if (s == 0) {
           cam.d = P.cam_state[0];
           for (int k = 0; k < 5; ++k) cam.v[k] = P.cam_state[1 + k];
+        } else if constexpr (parks<F>()) {
+          cam.d = lk[0];
+          for (int k = 0; k < 5; ++k) cam.v[k] = lk[(1 + k) * LB];
         }
         const float u = ((float)i + rtx::uniform(loc)) / (float)P.W;
         const float v = ((float)j + rtx::uniform(loc)) / (float)P.H;
@@ -1397,6 +1439,10 @@ void render_kernel(const RenderParams P) {
         ray.d = ld3(C.lower_left) + u * ld3(C.horizontal) + v * ld3(C.vertical) - ld3(C.origin) - off;
         ray.tm = urange(cr, C.time0, C.time1);
         att = mk(1.0f, 1.0f, 1.0f);
+        if constexpr (parks<F>()) {
+          lk[0] = cam.d;
+          for (int k = 0; k < 5; ++k) lk[(1 + k) * LB] = cam.v[k];
+        }
       }
 
       // ---- one segment (render.h:60-77)
@@ -1444,11 +1490,21 @@ void render_kernel(const RenderParams P) {
         }
       }
       if (ended) {
+        if constexpr (parks<F>()) col = mk(__uint_as_float(lk[6 * LB]), __uint_as_float(lk[7 * LB]), __uint_as_float(lk[8 * LB]));
         col = col + contrib;
+        if constexpr (parks<F>()) {
+          lk[6 * LB] = __float_as_uint(col.x);
+          lk[7 * LB] = __float_as_uint(col.y);
+          lk[8 * LB] = __float_as_uint(col.z);
+        }
         depth = 0;
         ++nsamp;
         if (++s == P.spp) {
           const V out = (1.0f / (float)P.spp) * col;
+          if constexpr (parks<F>()) {
+            f = (int)lk[9 * LB];
+            r = (int)lk[10 * LB];
+          }
           float* dst = P.fb + 3 * (((long long)f * P.rows + r) * P.W + i);
           dst[0] = out.x;
           dst[1] = out.y;
@@ -1842,6 +1898,9 @@ struct Variant {
 #define RT_VARIANT(m) {m, (const void*)render_kernel<m>}
 #define RT_VARIANT_STEP(m) {m, (const void*)render_step_kernel<m>}
 const Variant kVariants[] = {
+#ifdef RT_ONLY_MASK  // register-pressure experiments (scripts/isa_meta.py --only): one instantiation
+    RT_VARIANT(RT_ONLY_MASK),
+#else
     RT_VARIANT_STEP(F_SPHERES | F_LDS | F_STEP),
     RT_VARIANT_STEP(F_SPHERES | F_STEP),
     RT_VARIANT(F_SPHERES),
@@ -1863,6 +1922,7 @@ const Variant kVariants[] = {
     RT_VARIANT(F_MESH | F_STATS),
     RT_VARIANT(F_MESH | F_EXACT),
     RT_VARIANT(F_FINAL),
+#endif
 };
 #undef RT_VARIANT
 #undef RT_VARIANT_STEP
@@ -2156,7 +2216,7 @@ int rt_ctx_create(int hip_device, rt_ctx** out) {
     for (int v = 0; v < kNumVariants; ++v)
       chk(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->blocks_per_cu[v], kVariants[v].fn, variant_block(v),
                                                        (kVariants[v].mask & F_LDS) ? kLdsBudget
-                                                                                   : variant_block(v) * kStackDepth * 4),
+                                                                                   : variant_block(v) * (kStackDepth + kLocker) * 4),
           "occupancy");
   }
   if (rc != RT_OK) {
@@ -2432,7 +2492,7 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   P.S.lds_prims = lds_var ? c->dev_prims : 0;
   P.S.lds_mats = lds_var ? c->dev_mats : 0;
   P.S.lds_texs = lds_var ? c->dev_texs : 0;
-  const size_t shmem = lds_var ? lds_bytes + (size_t)bs * kStackDepth * 2 : (size_t)bs * kStackDepth * 4;
+  const size_t shmem = lds_var ? lds_bytes + (size_t)bs * kStackDepth * 2 : (size_t)bs * (kStackDepth + kLocker) * 4;
   const long long resident = (long long)c->cus * std::max(1, c->blocks_per_cu[var]);
   // Persistent grid: every resident workgroup, even when there are fewer items than lanes (a
   // rank of a multi-GPU run): waves take items dynamically, so the items spread over all CUs
