@@ -92,6 +92,7 @@ def parse():
     ap.add_argument("--exact", action="store_true", help="reference BVH visit set (no culling)")
     ap.add_argument("--no-lds", action="store_true", help="keep the scene in global memory")
     ap.add_argument("--no-step", action="store_true", help="segment-per-trip kernel even when the world is one BVH")
+    ap.add_argument("--no-bins", action="store_true", help="camera rays traverse the BVH (no per-tile candidate lists)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the untimed node/prim counting pass")
@@ -184,7 +185,7 @@ def main():
     cam = rt.RT_CAM_REF_SLOT0 if a.cam == "ref" else rt.RT_CAM_PER_PIXEL
     args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, band_rows=a.band_rows,
                         band_first=rank, band_stride=world, exact=a.exact, lds=not a.no_lds,
-                        step=not a.no_step)
+                        step=not a.no_step, bins=not a.no_bins)
     rows = rt.owned_rows(args)
     all_rows = []
     for r in range(world):

@@ -174,6 +174,8 @@ enum rt_cam_mode {
                                      kernel instead of the stepwise one (same pixels)           */
 #define RT_FLAG_NO_SCHEDULE 32    /* natural item order on every launch (no longest-first
                                      schedule from the previous launch; same pixels)            */
+#define RT_FLAG_NO_CAMERA_BINS 64 /* camera rays traverse the BVH instead of testing their 8x8
+                                     tile's candidate list (world = one BVH; same pixels)       */
 
 typedef struct rt_render_args {
   int32_t width, height;  /* full image size; N = width*height drives the RNG slots (H3)  */

@@ -1173,7 +1173,7 @@ static V3 trace(const ref_scene& s, Ray r, Draw& g, int depth) {
       const long long k = g_cap_n.fetch_add(1);
       if (k < g_cap_max) {
         float* e = g_cap + 8 * k;
-        e[0] = r.o.x; e[1] = r.o.y; e[2] = r.o.z; e[3] = r.d.x; e[4] = r.d.y; e[5] = r.d.z; e[6] = r.tm; e[7] = 0;
+        e[0] = r.o.x; e[1] = r.o.y; e[2] = r.o.z; e[3] = r.d.x; e[4] = r.d.y; e[5] = r.d.z; e[6] = r.tm; e[7] = (float)i;  // e[7]: bounce depth (0 = camera ray)
       }
     }
     if (!s.world->hit(r, 0.001f, INFINITY, rec, g)) return att * s.background;

@@ -629,6 +629,32 @@ __device__ bool bvh_exact(const DScene& S, int base, int rows, const Ray& r, V i
 // compare exactly, as bvh.h does (strictly smaller t, ties to the lower leaf rank), and the
 // loser is not kept in `second`: an exact loser of an exact winner has t >= the winner's t, so
 // when a range later displaces that winner, the winner's lo (added to `second`) covers it.
+// One candidate of the culled search (a primitive whose range test passed): the lane keeps the
+// candidate with the smallest lo as the winner [blo, bhi] and the smallest lo of every other
+// candidate in `second`.  Two exact candidates (lo = hi) compare exactly, as bvh.h does (strictly
+// smaller t, ties to the lower leaf rank), and the loser is not kept in `second`: an exact loser of
+// an exact winner has t >= the winner's t, so when a range later displaces that winner, the
+// winner's lo (added to `second`) covers it.
+__device__ __forceinline__ void take_candidate(float lo, float hi, int pi, int rk, float& blo, float& bhi,
+                                               float& second, int& best_prim, int& best_rank) {
+  if (lo == hi && blo == bhi) {  // both exact: the reference's rule, ties to the lower rank
+    if (lo < blo || (lo == blo && rk < best_rank)) {
+      blo = lo;
+      bhi = hi;
+      best_prim = pi;
+      best_rank = rk;
+    }
+  } else if (lo < blo) {
+    second = __builtin_fminf(second, blo);
+    blo = lo;
+    bhi = hi;
+    best_prim = pi;
+    best_rank = rk;
+  } else {
+    second = __builtin_fminf(second, lo);
+  }
+}
+
 template <int F>
 __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r, V oi, V finv, float a, float rcpa,
                                           float tmin, float tmax, int& cur, int& sp, float& blo, float& bhi,
@@ -655,25 +681,8 @@ __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r,
       const int pi = -ch - 1;
       const PrimRec q = load_prim<F>(S, pi);
       float lo, hi;
-      if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim)) {
-        const int rk = __float_as_int(q.c.y);
-        if (lo == hi && blo == bhi) {  // both exact: the reference's rule, ties to the lower rank
-          if (lo < blo || (lo == blo && rk < best_rank)) {
-            blo = lo;
-            bhi = hi;
-            best_prim = pi;
-            best_rank = rk;
-          }
-        } else if (lo < blo) {
-          second = __builtin_fminf(second, blo);
-          blo = lo;
-          bhi = hi;
-          best_prim = pi;
-          best_rank = rk;
-        } else {
-          second = __builtin_fminf(second, lo);
-        }
-      }
+      if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim))
+        take_candidate(lo, hi, pi, __float_as_int(q.c.y), blo, bhi, second, best_prim, best_rank);
       if (side == 0) hl = false; else hr = false;
       RT_STAMP(3);
     }
@@ -692,6 +701,24 @@ __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r,
   if (sp == 0) return false;
   cur = stk[BS * --sp];
   return true;
+}
+
+// Camera-ray candidates of a world BVH from the per-tile candidate list (bin_tiles_kernel): every
+// primitive that any camera ray of the 8x8-pixel tile can hit, over the lens disk and the shutter,
+// is in the list, so the candidates of the culled search are all tested here instead of traversing
+// the tree; bvh_settle then decides the query exactly as after a traversal.
+template <int F>
+__device__ __forceinline__ void tile_candidates(const DScene& S, const int32_t* __restrict__ ent, int cnt,
+                                                const Ray& r, float a, float rcpa, float tmin, float tmax,
+                                                float& blo, float& bhi, float& second, int& best_prim,
+                                                int& best_rank, unsigned& nprim) {
+  for (int k = 0; k < cnt; ++k) {
+    const int pi = ent[k];
+    const PrimRec q = load_prim<F>(S, pi);
+    float lo, hi;
+    if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim))
+      take_candidate(lo, hi, pi, __float_as_int(q.c.y), blo, bhi, second, best_prim, best_rank);
+  }
 }
 
 // Second half of bvh_closest once the candidate search has ended: overflow fallback, audit mode,
@@ -1279,6 +1306,11 @@ struct RenderParams {
   uint16_t* item_cost;
   unsigned long long n_long;
   uint32_t cam_state[6];
+  // Camera-ray candidate lists (render_step_kernel; null: camera rays traverse the tree): per 8x8
+  // tile of the image, tile_cnt[t] entries at tile_ent[t * tile_cap] (-1: the tile overflowed).
+  const int32_t* tile_cnt;
+  const int32_t* tile_ent;
+  int tiles_x, tile_cap;
 #ifdef RT_TRACE
   float* trace;
   long long trace_item;
@@ -1290,8 +1322,14 @@ struct RenderParams {
 
 constexpr int kBlock = 256;
 constexpr int kAuditCap = 4096;
+constexpr int kTileShift = 3;  // camera-ray candidate lists per 8x8-pixel tile
+constexpr int kTileCap = 32;   // entries per tile list (a fuller tile traverses the tree)
 constexpr int kRefill = 16;  // refill a wave once this many lanes are idle
 constexpr int kShadeMin = 60;  // render_step_kernel: default shading-phase threshold
+#ifndef RT_SHADE_PASSES
+#define RT_SHADE_PASSES 2
+#endif
+constexpr int kShadePasses = RT_SHADE_PASSES;  // render_step_kernel: shading passes per phase
 constexpr unsigned kChunk = 64;  // items a wave claims per work-counter atomic
 static_assert(kChunk >= 64, "claim_items: one claim must cover a refill of every lane of a wave");
 
@@ -1595,7 +1633,10 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
 #endif
 
   for (;;) {
-    {
+    // Shading passes: a camera ray answered by its tile's candidate list (mode 2 right after the
+    // setup) is shaded in another pass of the same phase, so the traversal loop that follows
+    // starts with every lane traversing.
+    for (int pass = 0;; ++pass) {
       RT_DIAG(2);
       // ---- shading phase: finish the ended queries (render.h:60-77)
       RT_STAMP(7);  // back-to-back pair: phase 7 = the cost of one stamp per loop trip
@@ -1719,10 +1760,20 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
         sp = 0;
         overflow = false;
         mode = 1;
+        if (depth == 0 && P.tile_cnt) {  // camera ray: the tile's candidate list instead of the tree
+          const int t = (j >> kTileShift) * P.tiles_x + (i >> kTileShift);
+          const int cnt = P.tile_cnt[t];
+          if (cnt >= 0) {
+            tile_candidates<F>(S, P.tile_ent + (size_t)t * P.tile_cap, cnt, ray, qa, rcpa, tmin, tmax, best, bhi,
+                               second, best_prim, best_rank, nprim);
+            mode = 2;
+          }
+        }
       }
+      if (pass + 1 >= kShadePasses || __ballot(mode == 2) == 0) break;
     }
     RT_STAMP(3);
-    if (__ballot(mode == 1) == 0) break;  // no item left for any lane of the wave
+    if (__ballot(mode != 0) == 0) break;  // no item left for any lane of the wave (mode 2: a listed camera ray)
     // ---- traversal steps until shade_min lanes wait (or none traverses)
     for (;;) {
       RT_DIAG(3);
@@ -1847,6 +1898,76 @@ __global__ __launch_bounds__(kBlock) void resolve_kernel(const float* __restrict
   out[k] = (uint8_t)quant(acc / (float)nfb);
 }
 
+// Camera-ray candidate lists: one thread per 8x8-pixel tile lists every primitive of the world BVH
+// that a camera ray of the tile may hit.  A camera ray (render.h:105-108, camera.h:49-58) is
+//   X(t) = O + off + t (F - O - off),  F = lower_left + u horizontal + v vertical,
+// with (u, v) inside the tile (jitter in [0, 1] of a pixel), |off| <= lens_radius = L and its time
+// in the shutter.  X(t) = Y(t) + (1 - t) off with Y(t) = O + t (F - O) inside the pinhole frustum of
+// the tile, so a sphere (C, R) hit at parameter t is within R + |1 - t| L of that frustum: it is
+// kept unless it lies farther than that outside one of the frustum's four side planes.  (C, R)
+// bounds the primitive's box over the shutter (rt_scene_upload), t <= (|C - O| + R + L) / (dmin - L)
+// with dmin the distance from O to the focus plane, and R is widened by 4e-3 (|C - O| + R + L) for
+// the float rounding of the ray and of the reference's hit tests (a sphere's discriminant admits
+// rays up to ~1e-3 |oc| beyond its radius).  Double precision throughout.
+__global__ __launch_bounds__(kBlock) void bin_tiles_kernel(const float4* __restrict__ sph, const int32_t* __restrict__ ids,
+                                                          int n, rt_camera cam, int W, int H, int tx, int ty,
+                                                          int32_t* __restrict__ cnt, int32_t* __restrict__ ent) {
+  const int t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= tx * ty) return;
+  const int i0 = (t % tx) << kTileShift, j0 = (t / tx) << kTileShift;
+  const int i1 = min(i0 + (1 << kTileShift), W), j1 = min(j0 + (1 << kTileShift), H);
+  const double us[2] = {(i0 - 0.01) / W, (i1 + 0.01) / W}, vs[2] = {(j0 - 0.01) / H, (j1 + 0.01) / H};
+  double O[3], D[4][3], Dc[3] = {0, 0, 0};
+  for (int k = 0; k < 3; ++k) O[k] = cam.origin[k];
+  const int cu[4] = {0, 1, 1, 0}, cv[4] = {0, 0, 1, 1};
+  for (int c = 0; c < 4; ++c)
+    for (int k = 0; k < 3; ++k) {
+      D[c][k] = (double)cam.lower_left[k] + us[cu[c]] * cam.horizontal[k] + vs[cv[c]] * cam.vertical[k] - O[k];
+      Dc[k] += 0.25 * D[c][k];
+    }
+  double N[4][3];
+  for (int c = 0; c < 4; ++c) {
+    const double* a = D[c];
+    const double* b = D[(c + 1) & 3];
+    double m[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+    const double len = sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+    const double sg = (m[0] * Dc[0] + m[1] * Dc[1] + m[2] * Dc[2]) < 0 ? -1.0 : 1.0;
+    for (int k = 0; k < 3; ++k) N[c][k] = sg * m[k] / len;
+  }
+  double nf[3];
+  {
+    const float* h = cam.horizontal;
+    const float* v = cam.vertical;
+    nf[0] = (double)h[1] * v[2] - (double)h[2] * v[1];
+    nf[1] = (double)h[2] * v[0] - (double)h[0] * v[2];
+    nf[2] = (double)h[0] * v[1] - (double)h[1] * v[0];
+    const double len = sqrt(nf[0] * nf[0] + nf[1] * nf[1] + nf[2] * nf[2]);
+    for (int k = 0; k < 3; ++k) nf[k] /= len;
+  }
+  const double dmin = fabs(D[0][0] * nf[0] + D[0][1] * nf[1] + D[0][2] * nf[2]);
+  const double L = (double)fabsf(cam.lens_radius) * (1.0 + 1e-5) + 1e-7;
+  int c = 0;
+  if (!(dmin > 2.0 * L) || !(dmin < 1e30)) {
+    c = kTileCap + 1;  // degenerate camera: no list
+  } else {
+    for (int q = 0; q < n; ++q) {
+      const float4 s = sph[q];
+      const double C[3] = {s.x - O[0], s.y - O[1], s.z - O[2]};
+      const double dist = sqrt(C[0] * C[0] + C[1] * C[1] + C[2] * C[2]);
+      const double reach = dist + s.w + L;
+      const double tmax = reach / (dmin - L);
+      const double m = s.w + 4e-3 * reach + L * fmax(1.0, tmax) + 1e-6;
+      bool in = m == m;  // NaN bound (non-finite primitive): always listed
+      for (int p = 0; p < 4 && in; ++p) in = N[p][0] * C[0] + N[p][1] * C[1] + N[p][2] * C[2] >= -m;
+      if (in || !(m == m)) {
+        if (c < kTileCap) ent[(size_t)t * kTileCap + c] = ids[q];
+        ++c;
+      }
+    }
+  }
+  cnt[t] = c <= kTileCap ? c : -1;
+}
+
 }  // namespace
 
 // ====================================================================== host side (C ABI)
@@ -1887,6 +2008,14 @@ struct rt_ctx {
   float last_ms = 0.0f;
   char last_kernel[48] = "";  // rocprof name stem of the last render launch, e.g. render_step_kernel<25730>
   float* dbg = nullptr;  // audit log: [0] = count, then 16 floats per entry
+  // Camera-ray candidate lists (world = one BVH): bounding spheres of the world BVH's primitives
+  // over the shutter (scene buffers) and the per-tile lists of the last (scene, W, H).
+  const float4* bin_sph = nullptr;
+  const int32_t* bin_ids = nullptr;
+  int bin_n = 0;
+  int32_t* tiles = nullptr;  // [ntiles] counts, then [ntiles * kTileCap] entries
+  long long tiles_cap = 0;
+  long long tiles_key[3] = {-1, -1, -1};
 };
 
 namespace {
@@ -1898,7 +2027,9 @@ struct Variant {
 #define RT_VARIANT(m) {m, (const void*)render_kernel<m>}
 #define RT_VARIANT_STEP(m) {m, (const void*)render_step_kernel<m>}
 const Variant kVariants[] = {
-#ifdef RT_ONLY_MASK  // register-pressure experiments (scripts/isa_meta.py --only): one instantiation
+#if defined(RT_ONLY_MASK) && defined(RT_ONLY_STEP)  // ISA experiments: one stepwise instantiation
+    RT_VARIANT_STEP(RT_ONLY_MASK),
+#elif defined(RT_ONLY_MASK)  // register-pressure experiments (scripts/isa_meta.py --only): one instantiation
     RT_VARIANT(RT_ONLY_MASK),
 #else
     RT_VARIANT_STEP(F_SPHERES | F_LDS | F_STEP),
@@ -2241,6 +2372,7 @@ int rt_ctx_destroy(rt_ctx* c) {
   if (c->item_cost) (void)hipFree(c->item_cost);
   if (c->perm) (void)hipFree(c->perm);
   if (c->dbg) (void)hipFree(c->dbg);
+  if (c->tiles) (void)hipFree(c->tiles);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2346,6 +2478,33 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   d.bg[2] = s->background[2];
   c->features = scene_features(s);
   c->world_bvh = s->n_world == 1 && s->objects[s->world[0]].kind == RT_OBJ_BVH;
+  c->bin_sph = nullptr;
+  c->bin_ids = nullptr;
+  c->bin_n = 0;
+  if (c->world_bvh) {  // bounding spheres of the world BVH's primitives (boxes over the shutter)
+    const rt_object& o = s->objects[s->world[0]];
+    const int inner = (1 << o.b) - 1, last0 = (1 << (o.b - 1)) - 1;
+    const float t0 = s->camera.time0, t1 = s->camera.time1;
+    std::vector<float4> sph;
+    std::vector<int32_t> ids;
+    for (int k = last0; k < inner; ++k)
+      for (int id : {s->nodes[o.a + k].leaf_a, s->nodes[o.a + k].leaf_b}) {
+        if (id < 0) continue;
+        const rth::Box b = rth::prim_box(prims[id], s->triangles, t0 < t1 ? t0 : t1, t0 < t1 ? t1 : t0);
+        double cx = 0.5 * ((double)b.lo[0] + b.hi[0]), cy = 0.5 * ((double)b.lo[1] + b.hi[1]),
+               cz = 0.5 * ((double)b.lo[2] + b.hi[2]);
+        const double hx = 0.5 * ((double)b.hi[0] - b.lo[0]), hy = 0.5 * ((double)b.hi[1] - b.lo[1]),
+                     hz = 0.5 * ((double)b.hi[2] - b.lo[2]);
+        // radius rounded up past the float rounding of the centre: the sphere contains the box
+        const double rad = std::sqrt(hx * hx + hy * hy + hz * hz) * (1.0 + 1e-6) +
+                           1e-6 * (std::fabs(cx) + std::fabs(cy) + std::fabs(cz)) + 1e-30;
+        sph.push_back(make_float4((float)cx, (float)cy, (float)cz, (float)(rad * (1.0 + 1e-6))));
+        ids.push_back(id);
+      }
+    if ((rc = upload(c, sph.data(), sph.size(), &c->bin_sph))) return rc;
+    if ((rc = upload(c, ids.data(), ids.size(), &c->bin_ids))) return rc;
+    c->bin_n = (int)ids.size();
+  }
   c->dev_nodes = (int)nodes.size();
   c->dev_prims = (int)prims.size();
   c->dev_mats = s->n_materials;
@@ -2493,6 +2652,29 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   P.S.lds_mats = lds_var ? c->dev_mats : 0;
   P.S.lds_texs = lds_var ? c->dev_texs : 0;
   const size_t shmem = lds_var ? lds_bytes + (size_t)bs * kStackDepth * 2 : (size_t)bs * (kStackDepth + kLocker) * 4;
+  // Camera-ray candidate lists for the stepwise kernel, built once per (scene, W, H).
+  if ((kVariants[var].mask & F_STEP) != 0 && c->bin_n > 0 && (a->flags & RT_FLAG_NO_CAMERA_BINS) == 0) {
+    const int tx = (a->width + (1 << kTileShift) - 1) >> kTileShift, ty = (a->height + (1 << kTileShift) - 1) >> kTileShift;
+    const long long nt = (long long)tx * ty;
+    const long long tkey[3] = {c->scene_gen, a->width, a->height};
+    if (!std::equal(tkey, tkey + 3, c->tiles_key)) {
+      if (nt * (kTileCap + 1) > c->tiles_cap) {
+        if (c->tiles) HIPCHK(c, hipFree(c->tiles));
+        c->tiles = nullptr;
+        c->tiles_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->tiles, (size_t)nt * (kTileCap + 1) * sizeof(int32_t)));
+        c->tiles_cap = nt * (kTileCap + 1);
+      }
+      bin_tiles_kernel<<<(unsigned)((nt + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
+          c->bin_sph, c->bin_ids, c->bin_n, c->scene.cam, a->width, a->height, tx, ty, c->tiles, c->tiles + nt);
+      HIPCHK(c, hipGetLastError());
+      std::copy(tkey, tkey + 3, c->tiles_key);
+    }
+    P.tile_cnt = c->tiles;
+    P.tile_ent = c->tiles + nt;
+    P.tiles_x = tx;
+    P.tile_cap = kTileCap;
+  }
   const long long resident = (long long)c->cus * std::max(1, c->blocks_per_cu[var]);
   // Persistent grid: every resident workgroup, even when there are fewer items than lanes (a
   // rank of a multi-GPU run): waves take items dynamically, so the items spread over all CUs
