@@ -1110,8 +1110,10 @@ __device__ void object_record(const DScene& S, int oi, int prim, const Ray& r, f
 }
 
 // World = hittable_list of top-level objects (render.h:63 with t in [0.001, inf)).
+// mask: bit w clear = no ray of this query's set can reach entry w (w < 32; camera-ray tile masks).
 template <int F>
-__device__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+__device__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall,
+                          uint32_t mask) {
   float closest = __builtin_inff();
   // The widest variants (media and triangles: C5's) keep a record per closer entry: deferring
   // raises their spills at the 128-VGPR floor (C5 67 -> 85 ms); C3 28.6 -> 21.8 ms with it.
@@ -1123,6 +1125,7 @@ __device__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsig
   if constexpr (!defer) {
     bool any = false;
     for (int w = 0; w < S.n_world; ++w) {
+      if (w < 32 && ((mask >> w) & 1u) == 0) continue;
       Hit tmp;
       if (object_hit<F>(S, S.world[w], r, 0.001f, closest, tmp, rng, nnode, nprim, nfall)) {
         any = true;
@@ -1134,6 +1137,7 @@ __device__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsig
   } else {
     int wobj = -1, wprim = -1;
     for (int w = 0; w < S.n_world; ++w) {
+      if (w < 32 && ((mask >> w) & 1u) == 0) continue;
       float t;
       int pr;
       const int oi = S.world[w];
@@ -1311,6 +1315,9 @@ struct RenderParams {
   const int32_t* tile_cnt;
   const int32_t* tile_ent;
   int tiles_x, tile_cap;
+  // Camera-ray entry masks (render_kernel, list worlds; null: every entry is tested): bit w of
+  // tile_mask[t] = a camera ray of tile t may hit top-level entry w.
+  const uint32_t* tile_mask;
 #ifdef RT_TRACE
   float* trace;
   long long trace_item;
@@ -1495,7 +1502,9 @@ void render_kernel(const RenderParams P) {
   #endif
       RT_STAMP(2);
       RT_DIAG(2);
-      const bool hit_any = world_hit<F>(S, ray, h, loc, nnode, nprim, nfall);
+      const uint32_t wmask = (depth == 0 && P.tile_mask) ? P.tile_mask[(j >> kTileShift) * P.tiles_x + (i >> kTileShift)]
+                                                         : 0xffffffffu;
+      const bool hit_any = world_hit<F>(S, ray, h, loc, nnode, nprim, nfall, wmask);
       RT_STAMP(6);
   #ifdef RT_TRACE
       if (item == P.trace_item && P.trace) {
@@ -1898,74 +1907,99 @@ __global__ __launch_bounds__(kBlock) void resolve_kernel(const float* __restrict
   out[k] = (uint8_t)quant(acc / (float)nfb);
 }
 
-// Camera-ray candidate lists: one thread per 8x8-pixel tile lists every primitive of the world BVH
-// that a camera ray of the tile may hit.  A camera ray (render.h:105-108, camera.h:49-58) is
+// Camera-ray culling per 8x8-pixel tile.  A camera ray (render.h:105-108, camera.h:49-58) is
 //   X(t) = O + off + t (F - O - off),  F = lower_left + u horizontal + v vertical,
 // with (u, v) inside the tile (jitter in [0, 1] of a pixel), |off| <= lens_radius = L and its time
 // in the shutter.  X(t) = Y(t) + (1 - t) off with Y(t) = O + t (F - O) inside the pinhole frustum of
-// the tile, so a sphere (C, R) hit at parameter t is within R + |1 - t| L of that frustum: it is
-// kept unless it lies farther than that outside one of the frustum's four side planes.  (C, R)
-// bounds the primitive's box over the shutter (rt_scene_upload), t <= (|C - O| + R + L) / (dmin - L)
-// with dmin the distance from O to the focus plane, and R is widened by 4e-3 (|C - O| + R + L) for
-// the float rounding of the ray and of the reference's hit tests (a sphere's discriminant admits
-// rays up to ~1e-3 |oc| beyond its radius).  Double precision throughout.
+// the tile, so a sphere (C, R) hit at parameter t >= 0 is within R + |1 - t| L of that frustum: it
+// is kept unless it lies farther than that outside one of the frustum's four side planes.  (C, R)
+// bounds a primitive's or an object's box over the shutter (rt_scene_upload); t <= (|C - O| + R +
+// L) / (dmin - L) with dmin the distance from O to the focus plane; R is widened by 4e-3 (|C - O| +
+// R + L) for the float rounding of the ray and of the reference's hit tests (a sphere's
+// discriminant admits rays up to ~1e-3 |oc| beyond its radius).  Double precision throughout.
+struct TileFrustum {
+  double O[3], N[4][3], dmin, L;
+  bool ok;
+  __device__ void init(const rt_camera& cam, int W, int H, int t, int tx) {
+    const int i0 = (t % tx) << kTileShift, j0 = (t / tx) << kTileShift;
+    const int i1 = min(i0 + (1 << kTileShift), W), j1 = min(j0 + (1 << kTileShift), H);
+    const double us[2] = {(i0 - 0.01) / W, (i1 + 0.01) / W}, vs[2] = {(j0 - 0.01) / H, (j1 + 0.01) / H};
+    double D[4][3], Dc[3] = {0, 0, 0};
+    for (int k = 0; k < 3; ++k) O[k] = cam.origin[k];
+    const int cu[4] = {0, 1, 1, 0}, cv[4] = {0, 0, 1, 1};
+    for (int c = 0; c < 4; ++c)
+      for (int k = 0; k < 3; ++k) {
+        D[c][k] = (double)cam.lower_left[k] + us[cu[c]] * cam.horizontal[k] + vs[cv[c]] * cam.vertical[k] - O[k];
+        Dc[k] += 0.25 * D[c][k];
+      }
+    for (int c = 0; c < 4; ++c) {
+      const double* a = D[c];
+      const double* b = D[(c + 1) & 3];
+      const double m[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+      const double len = sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+      const double sg = (m[0] * Dc[0] + m[1] * Dc[1] + m[2] * Dc[2]) < 0 ? -1.0 : 1.0;
+      for (int k = 0; k < 3; ++k) N[c][k] = sg * m[k] / len;
+    }
+    const float* h = cam.horizontal;
+    const float* v = cam.vertical;
+    double nf[3] = {(double)h[1] * v[2] - (double)h[2] * v[1], (double)h[2] * v[0] - (double)h[0] * v[2],
+                    (double)h[0] * v[1] - (double)h[1] * v[0]};
+    const double nl = sqrt(nf[0] * nf[0] + nf[1] * nf[1] + nf[2] * nf[2]);
+    dmin = fabs(D[0][0] * nf[0] + D[0][1] * nf[1] + D[0][2] * nf[2]) / nl;
+    L = (double)fabsf(cam.lens_radius) * (1.0 + 1e-5) + 1e-7;
+    ok = dmin > 2.0 * L && dmin < 1e30;  // else (degenerate camera) no culling
+    for (int c = 0; c < 4; ++c)
+      for (int k = 0; k < 3; ++k) ok = ok && N[c][k] == N[c][k];
+  }
+  // May a camera ray of the tile hit something inside sphere s (xyz centre, w radius)?
+  __device__ bool sees(float4 s) const {
+    const double C[3] = {s.x - O[0], s.y - O[1], s.z - O[2]};
+    const double dist = sqrt(C[0] * C[0] + C[1] * C[1] + C[2] * C[2]);
+    const double reach = dist + s.w + L;
+    const double m = s.w + 4e-3 * reach + L * fmax(1.0, reach / (dmin - L)) + 1e-6;
+    if (!(m < 1e300)) return true;  // NaN or infinite bound: always kept
+    for (int p = 0; p < 4; ++p)
+      if (N[p][0] * C[0] + N[p][1] * C[1] + N[p][2] * C[2] < -m) return false;
+    return true;
+  }
+};
+
+// World = one BVH: every primitive of the BVH that a camera ray of tile t may hit (ids[q] for the
+// bounding sphere sph[q]); cnt[t] = -1 when the tile overflows kTileCap (it traverses the tree).
 __global__ __launch_bounds__(kBlock) void bin_tiles_kernel(const float4* __restrict__ sph, const int32_t* __restrict__ ids,
                                                           int n, rt_camera cam, int W, int H, int tx, int ty,
                                                           int32_t* __restrict__ cnt, int32_t* __restrict__ ent) {
   const int t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= tx * ty) return;
-  const int i0 = (t % tx) << kTileShift, j0 = (t / tx) << kTileShift;
-  const int i1 = min(i0 + (1 << kTileShift), W), j1 = min(j0 + (1 << kTileShift), H);
-  const double us[2] = {(i0 - 0.01) / W, (i1 + 0.01) / W}, vs[2] = {(j0 - 0.01) / H, (j1 + 0.01) / H};
-  double O[3], D[4][3], Dc[3] = {0, 0, 0};
-  for (int k = 0; k < 3; ++k) O[k] = cam.origin[k];
-  const int cu[4] = {0, 1, 1, 0}, cv[4] = {0, 0, 1, 1};
-  for (int c = 0; c < 4; ++c)
-    for (int k = 0; k < 3; ++k) {
-      D[c][k] = (double)cam.lower_left[k] + us[cu[c]] * cam.horizontal[k] + vs[cv[c]] * cam.vertical[k] - O[k];
-      Dc[k] += 0.25 * D[c][k];
-    }
-  double N[4][3];
-  for (int c = 0; c < 4; ++c) {
-    const double* a = D[c];
-    const double* b = D[(c + 1) & 3];
-    double m[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
-    const double len = sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
-    const double sg = (m[0] * Dc[0] + m[1] * Dc[1] + m[2] * Dc[2]) < 0 ? -1.0 : 1.0;
-    for (int k = 0; k < 3; ++k) N[c][k] = sg * m[k] / len;
-  }
-  double nf[3];
-  {
-    const float* h = cam.horizontal;
-    const float* v = cam.vertical;
-    nf[0] = (double)h[1] * v[2] - (double)h[2] * v[1];
-    nf[1] = (double)h[2] * v[0] - (double)h[0] * v[2];
-    nf[2] = (double)h[0] * v[1] - (double)h[1] * v[0];
-    const double len = sqrt(nf[0] * nf[0] + nf[1] * nf[1] + nf[2] * nf[2]);
-    for (int k = 0; k < 3; ++k) nf[k] /= len;
-  }
-  const double dmin = fabs(D[0][0] * nf[0] + D[0][1] * nf[1] + D[0][2] * nf[2]);
-  const double L = (double)fabsf(cam.lens_radius) * (1.0 + 1e-5) + 1e-7;
+  TileFrustum fr;
+  fr.init(cam, W, H, t, tx);
   int c = 0;
-  if (!(dmin > 2.0 * L) || !(dmin < 1e30)) {
-    c = kTileCap + 1;  // degenerate camera: no list
+  if (!fr.ok) {
+    c = kTileCap + 1;
   } else {
-    for (int q = 0; q < n; ++q) {
-      const float4 s = sph[q];
-      const double C[3] = {s.x - O[0], s.y - O[1], s.z - O[2]};
-      const double dist = sqrt(C[0] * C[0] + C[1] * C[1] + C[2] * C[2]);
-      const double reach = dist + s.w + L;
-      const double tmax = reach / (dmin - L);
-      const double m = s.w + 4e-3 * reach + L * fmax(1.0, tmax) + 1e-6;
-      bool in = m == m;  // NaN bound (non-finite primitive): always listed
-      for (int p = 0; p < 4 && in; ++p) in = N[p][0] * C[0] + N[p][1] * C[1] + N[p][2] * C[2] >= -m;
-      if (in || !(m == m)) {
+    for (int q = 0; q < n; ++q)
+      if (fr.sees(sph[q])) {
         if (c < kTileCap) ent[(size_t)t * kTileCap + c] = ids[q];
         ++c;
       }
-    }
   }
   cnt[t] = c <= kTileCap ? c : -1;
+}
+
+// World = a list: bit w of mask[t] is set when a camera ray of tile t may hit top-level entry w
+// (w < 32; entries past 32 are always tested).  An entry that no ray of the tile can reach makes
+// no RNG draw either: a constant medium draws only after its boundary is hit at t > t_min.
+__global__ __launch_bounds__(kBlock) void bin_masks_kernel(const float4* __restrict__ sph, int n, rt_camera cam, int W,
+                                                          int H, int tx, int ty, uint32_t* __restrict__ mask) {
+  const int t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= tx * ty) return;
+  TileFrustum fr;
+  fr.init(cam, W, H, t, tx);
+  uint32_t m = 0xffffffffu;
+  if (fr.ok)
+    for (int w = 0; w < n && w < 32; ++w)
+      if (!fr.sees(sph[w])) m &= ~(1u << w);
+  mask[t] = m;
 }
 
 }  // namespace
@@ -2393,6 +2427,81 @@ int32_t rt_owned_rows(const rt_render_args* a, int32_t* rows) {
   return n;
 }
 
+// Bounding sphere (centre, radius) of a primitive box, rounded outward so that it contains the box.
+float4 box_sphere(const rth::Box& b) {
+  const double cx = 0.5 * ((double)b.lo[0] + b.hi[0]), cy = 0.5 * ((double)b.lo[1] + b.hi[1]),
+               cz = 0.5 * ((double)b.lo[2] + b.hi[2]);
+  const double hx = 0.5 * ((double)b.hi[0] - b.lo[0]), hy = 0.5 * ((double)b.hi[1] - b.lo[1]),
+               hz = 0.5 * ((double)b.hi[2] - b.lo[2]);
+  const double rad = std::sqrt(hx * hx + hy * hy + hz * hz) * (1.0 + 1e-6) +
+                     1e-6 * (std::fabs(cx) + std::fabs(cy) + std::fabs(cz)) + 1e-30;
+  return make_float4((float)cx, (float)cy, (float)cz, (float)(rad * (1.0 + 1e-6)));
+}
+// Geometric box of a primitive over the shutter: bounding_box() (rth::prim_box) except for the
+// xz_rect, whose reference box spans z1 only (aarect.h:39, H4) and so does not bound the rect.
+rth::Box geom_box(const rt_prim& q, const rt_triangle* tris, float t0, float t1) {
+  rth::Box b = rth::prim_box(q, tris, t0, t1);
+  if ((q.type & 0xff) == RT_PRIM_RECT_XZ) {
+    b.lo[2] = std::fmin(q.p[2], q.p[3]);
+    b.hi[2] = std::fmax(q.p[2], q.p[3]);
+  }
+  return b;
+}
+// World-space box over the shutter [t0, t1] of object oi (an instance's child box through its
+// rotate_y + translate, a medium's boundary); false when it cannot be bounded.
+bool object_box(const rt_scene_soa* s, int oi, float t0, float t1, rth::Box& out, int depth = 0) {
+  const rt_prim* prims = s->prims;  // the scene's records (the device copies hold triangle operands)
+  if (oi < 0 || oi >= s->n_objects || depth > 8) return false;
+  const rt_object& o = s->objects[oi];
+  auto pbox = [&](int id) { return geom_box(prims[id], s->triangles, t0, t1); };
+  switch (o.kind) {
+    case RT_OBJ_PRIM:
+      out = pbox(o.a);
+      return true;
+    case RT_OBJ_LIST:
+      if (o.b <= 0) return false;
+      out = pbox(o.a);
+      for (int k = 1; k < o.b; ++k) out = rth::join(out, pbox(o.a + k));
+      return true;
+    case RT_OBJ_BVH: {
+      const int inner = (1 << o.b) - 1, last0 = (1 << (o.b - 1)) - 1;
+      bool any = false;
+      for (int k = last0; k < inner; ++k)
+        for (int id : {s->nodes[o.a + k].leaf_a, s->nodes[o.a + k].leaf_b}) {
+          if (id < 0) continue;
+          out = any ? rth::join(out, pbox(id)) : pbox(id);
+          any = true;
+        }
+      return any;
+    }
+    case RT_OBJ_MEDIUM:
+      return object_box(s, o.a, t0, t1, out, depth + 1);
+    case RT_OBJ_XFORM: {
+      rth::Box cb;
+      if (!object_box(s, o.a, t0, t1, cb, depth + 1)) return false;
+      // world = R^-1 (object) + offset, R^-1: x = c x' + s z', z = -s x' + c z' (hittable.h:112-143)
+      const double sn = (o.b & 2) ? o.f[3] : 0.0, cs = (o.b & 2) ? o.f[4] : 1.0;
+      const double off[3] = {(o.b & 1) ? o.f[0] : 0.0, (o.b & 1) ? o.f[1] : 0.0, (o.b & 1) ? o.f[2] : 0.0};
+      double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+      for (int q = 0; q < 8; ++q) {
+        const double x = (q & 1) ? cb.hi[0] : cb.lo[0], y = (q & 2) ? cb.hi[1] : cb.lo[1], z = (q & 4) ? cb.hi[2] : cb.lo[2];
+        const double w[3] = {cs * x + sn * z + off[0], y + off[1], -sn * x + cs * z + off[2]};
+        for (int k = 0; k < 3; ++k) {
+          lo[k] = std::min(lo[k], w[k]);
+          hi[k] = std::max(hi[k], w[k]);
+        }
+      }
+      for (int k = 0; k < 3; ++k) {  // widened for the float rounding of the instance transform
+        const double pad = 1e-5 * (std::fabs(lo[k]) + std::fabs(hi[k]) + (hi[k] - lo[k])) + 1e-6;
+        out.lo[k] = (float)(lo[k] - pad);
+        out.hi[k] = (float)(hi[k] + pad);
+      }
+      return true;
+    }
+  }
+  return false;
+}
+
 int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   if (c) ++c->scene_gen;  // invalidates the row-cost schedule
   if (!c || !s) return RT_ERR_ARG;
@@ -2490,20 +2599,22 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
     for (int k = last0; k < inner; ++k)
       for (int id : {s->nodes[o.a + k].leaf_a, s->nodes[o.a + k].leaf_b}) {
         if (id < 0) continue;
-        const rth::Box b = rth::prim_box(prims[id], s->triangles, t0 < t1 ? t0 : t1, t0 < t1 ? t1 : t0);
-        double cx = 0.5 * ((double)b.lo[0] + b.hi[0]), cy = 0.5 * ((double)b.lo[1] + b.hi[1]),
-               cz = 0.5 * ((double)b.lo[2] + b.hi[2]);
-        const double hx = 0.5 * ((double)b.hi[0] - b.lo[0]), hy = 0.5 * ((double)b.hi[1] - b.lo[1]),
-                     hz = 0.5 * ((double)b.hi[2] - b.lo[2]);
-        // radius rounded up past the float rounding of the centre: the sphere contains the box
-        const double rad = std::sqrt(hx * hx + hy * hy + hz * hz) * (1.0 + 1e-6) +
-                           1e-6 * (std::fabs(cx) + std::fabs(cy) + std::fabs(cz)) + 1e-30;
-        sph.push_back(make_float4((float)cx, (float)cy, (float)cz, (float)(rad * (1.0 + 1e-6))));
+        sph.push_back(box_sphere(geom_box(s->prims[id], s->triangles, t0 < t1 ? t0 : t1, t0 < t1 ? t1 : t0)));
         ids.push_back(id);
       }
     if ((rc = upload(c, sph.data(), sph.size(), &c->bin_sph))) return rc;
     if ((rc = upload(c, ids.data(), ids.size(), &c->bin_ids))) return rc;
     c->bin_n = (int)ids.size();
+  } else {  // list world: bounding spheres of the top-level entries (camera-ray entry masks)
+    const float t0 = s->camera.time0, t1 = s->camera.time1;
+    std::vector<float4> sph;
+    for (int w = 0; w < s->n_world && w < 32; ++w) {
+      rth::Box b;
+      sph.push_back(object_box(s, s->world[w], t0 < t1 ? t0 : t1, t0 < t1 ? t1 : t0, b)
+                        ? box_sphere(b) : make_float4(0.0f, 0.0f, 0.0f, INFINITY));
+    }
+    if ((rc = upload(c, sph.data(), sph.size(), &c->bin_sph))) return rc;
+    c->bin_n = -(int)sph.size();  // negative: entry spheres (masks), not primitive spheres (lists)
   }
   c->dev_nodes = (int)nodes.size();
   c->dev_prims = (int)prims.size();
@@ -2652,10 +2763,32 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   P.S.lds_mats = lds_var ? c->dev_mats : 0;
   P.S.lds_texs = lds_var ? c->dev_texs : 0;
   const size_t shmem = lds_var ? lds_bytes + (size_t)bs * kStackDepth * 2 : (size_t)bs * (kStackDepth + kLocker) * 4;
-  // Camera-ray candidate lists for the stepwise kernel, built once per (scene, W, H).
-  if ((kVariants[var].mask & F_STEP) != 0 && c->bin_n > 0 && (a->flags & RT_FLAG_NO_CAMERA_BINS) == 0) {
-    const int tx = (a->width + (1 << kTileShift) - 1) >> kTileShift, ty = (a->height + (1 << kTileShift) - 1) >> kTileShift;
-    const long long nt = (long long)tx * ty;
+  // Camera-ray culling, built once per (scene, W, H): candidate lists for the stepwise kernel
+  // (world = one BVH), top-level entry masks for list worlds.  Not in the exact / audit modes,
+  // whose counters are the reference's.
+  const int vm = kVariants[var].mask;
+  const bool cull = (a->flags & RT_FLAG_NO_CAMERA_BINS) == 0 && (vm & (F_EXACT | F_CHECK)) == 0;
+  const int tx = (a->width + (1 << kTileShift) - 1) >> kTileShift, ty = (a->height + (1 << kTileShift) - 1) >> kTileShift;
+  const long long nt = (long long)tx * ty;
+  if (cull && (vm & F_STEP) == 0 && c->bin_n < 0) {
+    const long long tkey[3] = {c->scene_gen, a->width, -1 - (long long)a->height};
+    if (!std::equal(tkey, tkey + 3, c->tiles_key)) {
+      if (nt > c->tiles_cap) {
+        if (c->tiles) HIPCHK(c, hipFree(c->tiles));
+        c->tiles = nullptr;
+        c->tiles_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->tiles, (size_t)nt * sizeof(int32_t)));
+        c->tiles_cap = nt;
+      }
+      bin_masks_kernel<<<(unsigned)((nt + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
+          c->bin_sph, -c->bin_n, c->scene.cam, a->width, a->height, tx, ty, (uint32_t*)c->tiles);
+      HIPCHK(c, hipGetLastError());
+      std::copy(tkey, tkey + 3, c->tiles_key);
+    }
+    P.tile_mask = (const uint32_t*)c->tiles;
+    P.tiles_x = tx;
+  }
+  if (cull && (vm & F_STEP) != 0 && c->bin_n > 0) {
     const long long tkey[3] = {c->scene_gen, a->width, a->height};
     if (!std::equal(tkey, tkey + 3, c->tiles_key)) {
       if (nt * (kTileCap + 1) > c->tiles_cap) {
