@@ -255,7 +255,7 @@ using Rng = rtx::State;
 
 // vec3.h:129-141 (left-to-right argument order).
 __device__ __forceinline__ float urange(Rng& s, float lo, float hi) { return lo + (hi - lo) * rtx::uniform(s); }
-__device__ V in_unit_sphere(Rng& s) {
+__device__ __forceinline__ V in_unit_sphere(Rng& s) {
   V p;
   bool inside;
   do {
@@ -267,7 +267,7 @@ __device__ V in_unit_sphere(Rng& s) {
   } while (!inside);
   return p;
 }
-__device__ V in_unit_disk(Rng& s) {
+__device__ __forceinline__ V in_unit_disk(Rng& s) {
   V p;
   bool inside;
   do {
@@ -463,7 +463,7 @@ __device__ __forceinline__ bool prim_range(const DScene& S, const PrimRec& q, co
 
 // Full hit record of primitive pi at parameter t (the fields hit() sets on success).
 template <int F>
-__device__ void finalize(const DScene& S, int pi, const Ray& r, float tmin, float t, Hit& h) {
+__device__ __forceinline__ void finalize(const DScene& S, int pi, const Ray& r, float tmin, float t, Hit& h) {
   const PrimRec q = load_prim<F>(S, pi);
   const int tw = __float_as_int(q.c.z);
   const int type = tw & RT_PRIM_TYPE_MASK;
@@ -567,7 +567,7 @@ __device__ __forceinline__ bool fbox(float4 lo, float4 hi, V oi, V inv, float tm
 // of a node are tested from one 64-byte fetch (siblings are adjacent in heap order), halving the
 // chain of dependent loads; `pending` keeps, per level, whether a right child is still to visit.
 template <int F>
-__device__ bool bvh_exact(const DScene& S, int base, int rows, const Ray& r, V inv, float tmin, float tmax,
+__device__ __forceinline__ bool bvh_exact(const DScene& S, int base, int rows, const Ray& r, V inv, float tmin, float tmax,
                           float& best, int& best_prim, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   const int last0 = (1 << (rows - 1)) - 1;
   best = __builtin_inff();
@@ -672,19 +672,27 @@ __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r,
   bool hl = fbox(l0, l1, oi, finv, tmin, cut, tl);
   bool hr = fbox(r0, r1, oi, finv, tmin, cut, tr);
   const int c0 = __float_as_int(l0.w), c1 = __float_as_int(l1.w);
-  // primitive children are tested right away (leaves hold one primitive)
-  #pragma unroll
-  for (int side = 0; side < 2; ++side) {
-    const int ch = side == 0 ? c0 : c1;
-    if ((side == 0 ? hl : hr) && ch < 0) {
-      RT_STAMP(4);
-      const int pi = -ch - 1;
-      const PrimRec q = load_prim<F>(S, pi);
-      float lo, hi;
-      if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim))
-        take_candidate(lo, hi, pi, __float_as_int(q.c.y), blo, bhi, second, best_prim, best_rank);
-      if (side == 0) hl = false; else hr = false;
-      RT_STAMP(3);
+  // Primitive children are tested right away (leaves hold one primitive): one pass for the lanes
+  // with a hit leaf child on either side, a second only for lanes with two (the candidate kept does
+  // not depend on the order, see take_candidate).  3 % faster on C2 than a pass per side.
+  {
+    const bool la = hl && c0 < 0, lb = hr && c1 < 0;
+    const int p0 = la ? c0 : (lb ? c1 : 0);
+    const int p1 = (la && lb) ? c1 : 0;
+    if (la) hl = false;
+    if (lb) hr = false;
+    #pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int ch = pass == 0 ? p0 : p1;
+      if (ch < 0) {
+        RT_STAMP(4);
+        const int pi = -ch - 1;
+        const PrimRec q = load_prim<F>(S, pi);
+        float lo, hi;
+        if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim))
+          take_candidate(lo, hi, pi, __float_as_int(q.c.y), blo, bhi, second, best_prim, best_rank);
+        RT_STAMP(3);
+      }
     }
   }
   if (hl && hr) {
@@ -818,7 +826,7 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
 //     ancestor pass the reference slab test against [tmin, tmax].  If that check fails (a
 //     floating-point edge of the reference's own boxes), the query is re-run on the exact visit set.
 template <int F>
-__device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, float tmin, float tmax, float& best,
+__device__ __forceinline__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, float tmin, float tmax, float& best,
                             int& best_prim, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
   const int base = o.a, rows = o.b;
@@ -854,7 +862,7 @@ __device__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, f
 // Closest hit of a PRIM / LIST / BVH object: (t, prim).  LIST keeps the reference list rule:
 // shrinking t_max, later object wins ties (hittable_list.h:23-39).
 template <int F>
-__device__ bool leaf_closest(const DScene& S, const rt_object& o, const Ray& r, float tmin, float tmax, float& t,
+__device__ __forceinline__ bool leaf_closest(const DScene& S, const rt_object& o, const Ray& r, float tmin, float tmax, float& t,
                              int& prim, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   if constexpr ((F & F_BVH) != 0)
     if (o.kind == RT_OBJ_BVH) return bvh_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall);
@@ -892,7 +900,7 @@ __device__ __forceinline__ Ray xform_ray(const rt_object& o, const Ray& r, Ray& 
 
 // t of the closest hit of an object that may be an XFORM over a leaf object.
 template <int F>
-__device__ bool xform_closest_t(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t,
+__device__ __forceinline__ bool xform_closest_t(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t,
                                 unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   const rt_object o = S.objects[oi];
   int prim;
@@ -922,7 +930,7 @@ __device__ __forceinline__ bool sphere_boundary_no_hit(const DScene& S, int boun
 // -- the same float operations on the same operands as the two box_t calls.  Returns 0: the
 // first query missed, 1: the second missed, 2: t1 and t2 set.
 template <int F>
-__device__ int box_boundary_t12(const DScene& S, const rt_object& bo, const PrimRec& q, const Ray& r, float& t1,
+__device__ __forceinline__ int box_boundary_t12(const DScene& S, const rt_object& bo, const PrimRec& q, const Ray& r, float& t1,
                                 float& t2) {
   Ray moved;
   const Ray rr = bo.kind == RT_OBJ_XFORM ? xform_ray(bo, r, moved) : r;
@@ -988,59 +996,21 @@ __device__ __forceinline__ bool medium_boundary(const DScene& S, const rt_object
       }
     }
   }
-  if (!xform_closest_t<F>(S, o.a, r, -inf, inf, t1, nnode, nprim, nfall)) return false;
-  if (sphere_boundary_no_hit<F>(S, o.a, t1)) return false;
-  return xform_closest_t<F>(S, o.a, r, t1 + 0.0001f, inf, t2, nnode, nprim, nfall);
-}
-
-// hittable::hit of one top-level object with a complete record.
-template <int F>
-__device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, float tmax, Hit& h, Rng& rng,
-                           unsigned& nnode, unsigned& nprim, unsigned& nfall) {
-  const rt_object o = S.objects[oi];
-  float t;
-  int prim;
-  if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {  // translate(rotate_y(child)), hittable.h:37-59, 112-143
-      Ray moved;
-      const Ray rr = xform_ray(o, r, moved);
-      const rt_object c = S.objects[o.a];
-      if (!leaf_closest<F>(S, c, rr, tmin, tmax, t, prim, nnode, nprim, nfall)) return false;
-      finalize<F>(S, prim, rr, tmin, t, h);
-      if (o.b & 2) {
-        const float s = o.f[3], cs = o.f[4];
-        const V p = mk(cs * h.p.x + s * h.p.z, h.p.y, -s * h.p.x + cs * h.p.z);
-        const V n = mk(cs * h.n.x + s * h.n.z, h.n.y, -s * h.n.x + cs * h.n.z);
-        h.p = p;
-        set_face(h, rr, n);  // rotated-frame ray against the world-frame normal (H25)
-      }
-      if (o.b & 1) {
-        h.p = h.p + mk(o.f[0], o.f[1], o.f[2]);
-        set_face(h, moved, h.n);
-      }
-      return true;
+  // One call site for both queries, inlined: an out-of-line call makes the kernel copy its whole
+  // argument block to scratch (the callee takes the scene by reference) and reload the scene
+  // pointers from there on every use (C5: ~160 scratch loads in the kernel body).
+  float lo = -inf;
+  for (int q = 0; q < 2; ++q) {
+    float t;
+    if (!xform_closest_t<F>(S, o.a, r, lo, inf, t, nnode, nprim, nfall)) return false;
+    if (q == 1) {
+      t2 = t;
+      break;
+    }
+    t1 = t;
+    if (sphere_boundary_no_hit<F>(S, o.a, t1)) return false;
+    lo = t1 + 0.0001f;
   }
-  if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {  // constant_medium.h:34-70 (one RNG draw per qualifying query, H8)
-      float t1, t2;
-      if (!medium_boundary<F>(S, o, r, t1, t2, nnode, nprim, nfall)) return false;
-      if (t1 < tmin) t1 = tmin;
-      if (t2 > tmax) t2 = tmax;
-      if (t1 >= t2) return false;
-      if (t1 < 0) t1 = 0;
-      const float len = __builtin_sqrtf(len2(r.d));
-      const float inside = (t2 - t1) * len;
-      const float hd = o.f[0] * rtm::det_logf(rtx::uniform(rng));
-      if (hd > inside) return false;
-      h.t = t1 + hd / len;
-      h.p = r.o + h.t * r.d;
-      h.n = mk(1.0f, 0.0f, 0.0f);
-      h.front = true;
-      h.mat = o.b;
-      h.u = 0.0f;  // stale in the reference; defined as 0
-      h.v = 0.0f;
-      return true;
-  }
-  if (!leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall)) return false;
-  finalize<F>(S, prim, r, tmin, t, h);
   return true;
 }
 
@@ -1050,7 +1020,7 @@ __device__ bool object_hit(const DScene& S, int oi, const Ray& r, float tmin, fl
 // closer entry's record (hittable_list.h:23-39), but only the last copy survives and a record is
 // a pure function of (object, primitive, ray, t), so the result is the same bit for bit.
 template <int F>
-__device__ bool object_query(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t, int& prim,
+__device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t, int& prim,
                              Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   const rt_object o = S.objects[oi];
   if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {  // translate(rotate_y(child)), hittable.h:37-59, 112-143
@@ -1077,7 +1047,7 @@ __device__ bool object_query(const DScene& S, int oi, const Ray& r, float tmin, 
 }
 
 template <int F>
-__device__ void object_record(const DScene& S, int oi, int prim, const Ray& r, float tmin, float t, Hit& h) {
+__device__ __forceinline__ void object_record(const DScene& S, int oi, int prim, const Ray& r, float tmin, float t, Hit& h) {
   const rt_object o = S.objects[oi];
   if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {
       Ray moved;
@@ -1112,45 +1082,24 @@ __device__ void object_record(const DScene& S, int oi, int prim, const Ray& r, f
 // World = hittable_list of top-level objects (render.h:63 with t in [0.001, inf)).
 // mask: bit w clear = no ray of this query's set can reach entry w (w < 32; camera-ray tile masks).
 template <int F>
-__device__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall,
+__device__ __forceinline__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall,
                           uint32_t mask) {
   float closest = __builtin_inff();
-  // The widest variants (media and triangles: C5's) keep a record per closer entry: deferring
-  // raises their spills at the 128-VGPR floor (C5 67 -> 85 ms); C3 28.6 -> 21.8 ms with it.
-#ifdef RT_DEFER_ALL
-  constexpr bool defer = true;
-#else
-  constexpr bool defer = (F & (F_MEDIUM | F_TRI)) != (F_MEDIUM | F_TRI);
-#endif
-  if constexpr (!defer) {
-    bool any = false;
-    for (int w = 0; w < S.n_world; ++w) {
-      if (w < 32 && ((mask >> w) & 1u) == 0) continue;
-      Hit tmp;
-      if (object_hit<F>(S, S.world[w], r, 0.001f, closest, tmp, rng, nnode, nprim, nfall)) {
-        any = true;
-        closest = tmp.t;
-        h = tmp;
-      }
+  int wobj = -1, wprim = -1;
+  for (int w = 0; w < S.n_world; ++w) {
+    if (w < 32 && ((mask >> w) & 1u) == 0) continue;
+    float t;
+    int pr;
+    const int oi = S.world[w];
+    if (object_query<F>(S, oi, r, 0.001f, closest, t, pr, rng, nnode, nprim, nfall)) {
+      closest = t;
+      wobj = oi;
+      wprim = pr;
     }
-    return any;
-  } else {
-    int wobj = -1, wprim = -1;
-    for (int w = 0; w < S.n_world; ++w) {
-      if (w < 32 && ((mask >> w) & 1u) == 0) continue;
-      float t;
-      int pr;
-      const int oi = S.world[w];
-      if (object_query<F>(S, oi, r, 0.001f, closest, t, pr, rng, nnode, nprim, nfall)) {
-        closest = t;
-        wobj = oi;
-        wprim = pr;
-      }
-    }
-    if (wobj < 0) return false;
-    object_record<F>(S, wobj, wprim, r, 0.001f, closest, h);
-    return true;
   }
+  if (wobj < 0) return false;
+  object_record<F>(S, wobj, wprim, r, 0.001f, closest, h);
+  return true;
 }
 
 // ------------------------------------------------------------------ textures (texture.h, perlin.h)
@@ -1182,7 +1131,7 @@ __device__ float perlin_turb(const rt_perlin& P, V p, int depth) {
   return (float)__builtin_fabs(acc);
 }
 template <int F>
-__device__ V tex_leaf(const DScene& S, const rt_texture& T, float u, float v, V p) {
+__device__ __forceinline__ V tex_leaf(const DScene& S, const rt_texture& T, float u, float v, V p) {
   if constexpr ((F & F_NOISE) != 0) {
     if (T.type == RT_TEX_NOISE) {
       const float n = perlin_noise(S.perlins[T.a], T.scale * p);
@@ -1215,7 +1164,7 @@ __device__ V tex_leaf(const DScene& S, const rt_texture& T, float u, float v, V 
   return ld3(T.color);  // solid
 }
 template <int F>
-__device__ V tex_value(const DScene& S, int ti, float u, float v, V p) {
+__device__ __forceinline__ V tex_value(const DScene& S, int ti, float u, float v, V p) {
   const rt_texture T = texs_of<F>(S)[ti];
   if constexpr ((F & F_CHECKER) != 0) {
     if (T.type == RT_TEX_CHECKER) {  // texture.h:37-45: sin(10x) sin(10y) sin(10z) < 0 -> odd
@@ -1226,9 +1175,14 @@ __device__ V tex_value(const DScene& S, int ti, float u, float v, V p) {
 }
 
 // ------------------------------------------------------------------ materials (material.h)
-// Returns true when the path continues (att, scattered set).  em = emitted colour.
+// Returns true when the path continues: att set and the scattered ray written over `ray` in place
+// (origin h.p, time kept).  em = emitted colour.  The in-place write matters: with the query chain
+// inlined, a conditional whole-struct copy of a separately built scattered ray (`ray = sc` under
+// `if (scatter(...))`) was compiled into per-component selects of which some kept the incoming
+// ray's values (widest variants, isotropic scatter: origin x/z and direction x of the old ray;
+// found with scripts/diag_trace.py on cornell_smoke).
 template <int F>
-__device__ bool scatter(const DScene& S, const Ray& in, const Hit& h, V& att, Ray& out, V& em, Rng& rng) {
+__device__ __forceinline__ bool scatter(const DScene& S, Ray& ray, const Hit& h, V& att, V& em, Rng& rng) {
   const int4 m = mats_of<F>(S)[h.mat];
   const int mt = m.x;
   em = mk(0.0f, 0.0f, 0.0f);
@@ -1237,14 +1191,21 @@ __device__ bool scatter(const DScene& S, const Ray& in, const Hit& h, V& att, Ra
   // the wave run a single loop instead of one per material.
   V sp = mk(0.0f, 0.0f, 0.0f);
   if (mt == RT_MAT_LAMBERTIAN || mt == RT_MAT_METAL || mt == RT_MAT_ISOTROPIC) sp = in_unit_sphere(rng);
+  if (mt == RT_MAT_DIFFUSE_LIGHT) {  // material.h:115-121
+    em = tex_value<F>(S, m.y, h.u, h.v, h.p);
+    return false;
+  }
+  // The materials differ only in the scattered direction (and attenuation): one direction chosen
+  // per lane, then one write of the ray.
+  V dir = sp;  // isotropic, material.h:133-137
+  bool cont = true;
   if (mt == RT_MAT_DIELECTRIC) {  // material.h:64-104
     att = mk(1.0f, 1.0f, 1.0f);
     const float ir = __int_as_float(m.z);
     const float ratio = h.front ? (1.0f / ir) : ir;
-    const V ud = unit(in.d);
+    const V ud = unit(ray.d);
     const float c = __builtin_fminf(dot(neg(ud), h.n), 1.0f);
     const float sn = __builtin_sqrtf(1.0f - c * c);
-    V dir;
     bool refl = ratio * sn > 1.0f;
     if (!refl) {
       const float sr = (1.0f - ratio) / (1.0f + ratio);
@@ -1260,30 +1221,20 @@ __device__ bool scatter(const DScene& S, const Ray& in, const Hit& h, V& att, Ra
       const V par = (-__builtin_sqrtf(__builtin_fabsf(1.0f - len2(perp)))) * h.n;
       dir = perp + par;
     }
-    out = Ray{h.p, dir, in.tm};
-    return true;
+  } else {
+    att = tex_value<F>(S, m.y, h.u, h.v, h.p);  // albedo
+    if (mt == RT_MAT_LAMBERTIAN) {  // material.h:25-35
+      dir = h.n + unit(sp);
+      const float e = 1e-6f;
+      if (__builtin_fabsf(dir.x) < e && __builtin_fabsf(dir.y) < e && __builtin_fabsf(dir.z) < e) dir = h.n;
+    } else if (mt == RT_MAT_METAL) {  // material.h:50-55
+      const V ud = unit(ray.d);
+      dir = (ud - (2.0f * dot(ud, h.n)) * h.n) + __int_as_float(m.z) * sp;
+      cont = dot(dir, h.n) > 0;
+    }
   }
-  const V tex = tex_value<F>(S, m.y, h.u, h.v, h.p);  // albedo, or emission for diffuse_light
-  if (mt == RT_MAT_DIFFUSE_LIGHT) {  // material.h:115-121
-    em = tex;
-    return false;
-  }
-  // The other materials differ only in the scattered direction; one Ray write after the
-  // selection (a per-case struct store was miscompiled in the widest kernel variant: origin
-  // x/y taken from the incoming ray, see scripts/diag_trace.py).
-  V dir = sp;  // isotropic, material.h:133-137
-  bool cont = true;
-  if (mt == RT_MAT_LAMBERTIAN) {  // material.h:25-35
-    dir = h.n + unit(sp);
-    const float e = 1e-6f;
-    if (__builtin_fabsf(dir.x) < e && __builtin_fabsf(dir.y) < e && __builtin_fabsf(dir.z) < e) dir = h.n;
-  } else if (mt == RT_MAT_METAL) {  // material.h:50-55
-    const V ud = unit(in.d);
-    dir = (ud - (2.0f * dot(ud, h.n)) * h.n) + __int_as_float(m.z) * sp;
-    cont = dot(dir, h.n) > 0;
-  }
-  out = Ray{h.p, dir, in.tm};
-  att = tex;
+  ray.o = h.p;
+  ray.d = dir;
   return cont;
 }
 
@@ -1523,10 +1474,8 @@ void render_kernel(const RenderParams P) {
         ended = true;
       } else {
         V a, em;
-        Ray sc;
-        if (scatter<F>(S, ray, h, a, sc, em, loc)) {
+        if (scatter<F>(S, ray, h, a, em, loc)) {
           att = att * a;
-          ray = sc;
           if (++depth == P.max_depth) {
             contrib = mk(0.0f, 0.0f, 0.0f);
             ended = true;
@@ -1663,11 +1612,9 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
           Hit h;
           finalize<F>(S, best_prim, ray, tmin, best, h);
           V a, em;
-          Ray sc;
           RT_STAMP(6);
-          if (scatter<F>(S, ray, h, a, sc, em, loc)) {
+          if (scatter<F>(S, ray, h, a, em, loc)) {
             att = att * a;
-            ray = sc;
             if (++depth == P.max_depth) {
               contrib = mk(0.0f, 0.0f, 0.0f);
               ended = true;
