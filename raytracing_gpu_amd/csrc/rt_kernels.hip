@@ -89,6 +89,7 @@ struct DScene {
   int32_t lds_prims;     // F_LDS: primitive count staged (validation margins follow them)
   int32_t lds_mats;      // F_LDS: materials staged after the margins (one float4 each)
   int32_t lds_texs;      // F_LDS: textures staged after the materials (two float4 each; stacks follow)
+  const float4* cam_tab; // REF camera mode: lens offset (xyz) and time (w) of sample s (camera_ray)
   rt_camera cam;
   float bg[3];
 };
@@ -148,11 +149,11 @@ __device__ __forceinline__ stack_t<F>* stack_of(const DScene& S) {
 // (entry d of thread t at [d * block + t]) so a wave's pushes/pops hit 64 distinct banks.
 constexpr int kStackDepth = 16;
 // Per-lane "locker" of render_kernel's global-memory variants: cold per-item / per-sample state
-// (the camera RNG copy, the sample sum, the item's fb and row) kept in LDS after the stacks,
+// (the sample sum, the item's fb and row) kept in LDS after the stacks,
 // lane-interleaved (word k of thread t at [k * block + t]), instead of VGPRs: it is touched once
 // per sample, and without it the variants' live state spills to scratch inside the traversal
 // loops (F_FINAL: 744 B per lane, ~340 B of scratch stores per segment, missing L2).
-constexpr int kLocker = 12;
+constexpr int kLocker = 5;
 template <int F>
 constexpr bool parks() {
   return (F & F_LDS) == 0;
@@ -898,19 +899,6 @@ __device__ __forceinline__ Ray xform_ray(const rt_object& o, const Ray& r, Ray& 
   return rr;
 }
 
-// t of the closest hit of an object that may be an XFORM over a leaf object.
-template <int F>
-__device__ __forceinline__ bool xform_closest_t(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t,
-                                unsigned& nnode, unsigned& nprim, unsigned& nfall) {
-  const rt_object o = S.objects[oi];
-  int prim;
-  if (o.kind != RT_OBJ_XFORM) return leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall);
-  Ray moved;
-  const Ray rr = xform_ray(o, r, moved);
-  const rt_object c = S.objects[o.a];
-  return leaf_closest<F>(S, c, rr, tmin, tmax, t, prim, nnode, nprim, nfall);
-}
-
 // constant_medium::hit over a (moving) sphere boundary after its first boundary query returned
 // t1: sphere.h's second root is its first (H1), so the query from t1 + 1e-4 returns nothing or
 // t1 itself (when t1 + 1e-4 rounds to t1), and with t2 = t1 the clamps to [tmin, tmax] leave
@@ -972,45 +960,21 @@ __device__ __forceinline__ int box_boundary_t12(const DScene& S, const rt_object
   return 2;
 }
 
-// The two boundary queries of constant_medium::hit (constant_medium.h:38-44): t1 over (-inf, inf),
-// t2 from t1 + 1e-4.  Returns false when either misses (or, for a sphere boundary, when the second
-// query cannot hit: sphere_boundary_no_hit).  Primitive boundaries are answered inline: the
-// general path (xform_closest_t) stays out of line in the widest variants, and a call spills
-// every live VGPR of the kernel to scratch around it.
+// constant_medium::hit after its boundary queries (constant_medium.h:45-70): clamps, then one RNG
+// draw per qualifying query (H8).  prim = -1 marks a volume hit.
 template <int F>
-__device__ __forceinline__ bool medium_boundary(const DScene& S, const rt_object& o, const Ray& r, float& t1, float& t2,
-                                                unsigned& nnode, unsigned& nprim, unsigned& nfall) {
-  const float inf = __builtin_inff();
-  if constexpr ((F & F_STATS) == 0) {  // stats variants run the reference's two queries to count them
-    const rt_object bo = S.objects[o.a];
-    const bool prim_leaf = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].kind == RT_OBJ_PRIM : bo.kind == RT_OBJ_PRIM;
-    if (prim_leaf) {
-      const int pi = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].a : bo.a;
-      const PrimRec q = load_prim<F>(S, pi);
-      if ((F & F_RECT) != 0 && prim_type(q) == RT_PRIM_BOX) return box_boundary_t12<F>(S, bo, q, r, t1, t2) == 2;
-      if (bo.kind == RT_OBJ_PRIM) {
-        unsigned np = 0;
-        if (!prim_t_q<F>(S, q, r, -inf, inf, t1, np)) return false;
-        if (prim_type(q) <= RT_PRIM_MOVING_SPHERE && t1 == t1) return false;  // sphere_boundary_no_hit
-        return prim_t_q<F>(S, q, r, t1 + 0.0001f, inf, t2, np);
-      }
-    }
-  }
-  // One call site for both queries, inlined: an out-of-line call makes the kernel copy its whole
-  // argument block to scratch (the callee takes the scene by reference) and reload the scene
-  // pointers from there on every use (C5: ~160 scratch loads in the kernel body).
-  float lo = -inf;
-  for (int q = 0; q < 2; ++q) {
-    float t;
-    if (!xform_closest_t<F>(S, o.a, r, lo, inf, t, nnode, nprim, nfall)) return false;
-    if (q == 1) {
-      t2 = t;
-      break;
-    }
-    t1 = t;
-    if (sphere_boundary_no_hit<F>(S, o.a, t1)) return false;
-    lo = t1 + 0.0001f;
-  }
+__device__ __forceinline__ bool medium_hit(const rt_object& o, const Ray& r, float tmin, float tmax, float t1, float t2,
+                                           Rng& rng, float& t, int& prim) {
+  if (t1 < tmin) t1 = tmin;
+  if (t2 > tmax) t2 = tmax;
+  if (t1 >= t2) return false;
+  if (t1 < 0) t1 = 0;
+  const float len = __builtin_sqrtf(len2(r.d));
+  const float inside = (t2 - t1) * len;
+  const float hd = o.f[0] * rtm::det_logf(rtx::uniform(rng));
+  if (hd > inside) return false;
+  t = t1 + hd / len;
+  prim = -1;
   return true;
 }
 
@@ -1019,31 +983,85 @@ __device__ __forceinline__ bool medium_boundary(const DScene& S, const rt_object
 // record from them.  world_hit builds only the winning entry's record: the reference copies every
 // closer entry's record (hittable_list.h:23-39), but only the last copy survives and a record is
 // a pure function of (object, primitive, ray, t), so the result is the same bit for bit.
+// Every query of the object goes through ONE leaf query (one inlined copy of the BVH traversal
+// per kernel): a constant medium's two boundary queries (constant_medium.h:38-44: over (-inf, inf),
+// then from t1 + 1e-4; phases 0 and 1) and a plain object's own query (phase 2), each through an
+// optional translate/rotate_y (hittable.h:37-59, 112-143).  Primitive boundaries (C3's boxes, C5's
+// spheres) are answered before that, without a traversal.  The query chain is inlined: an
+// out-of-line call made the kernel copy its whole argument block to scratch and reload the scene
+// pointers from there on every use (C5: ~160 scratch loads in the kernel body).
 template <int F>
-__device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t, int& prim,
-                             Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+__device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t,
+                                             int& prim, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+  const float inf = __builtin_inff();
   const rt_object o = S.objects[oi];
-  if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {  // translate(rotate_y(child)), hittable.h:37-59, 112-143
-      Ray moved;
-      const Ray rr = xform_ray(o, r, moved);
-      return leaf_closest<F>(S, S.objects[o.a], rr, tmin, tmax, t, prim, nnode, nprim, nfall);
+  int phase = 2, target = oi;
+  float lo = tmin, hi = tmax, t1 = 0.0f;
+  if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {
+      if constexpr ((F & F_STATS) == 0) {  // stats variants run the reference's two queries to count them
+        const rt_object bo = S.objects[o.a];
+        const bool prim_leaf = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].kind == RT_OBJ_PRIM : bo.kind == RT_OBJ_PRIM;
+        if (prim_leaf) {
+          const int pi = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].a : bo.a;
+          const PrimRec q = load_prim<F>(S, pi);
+          float b1, b2;
+          if ((F & F_RECT) != 0 && prim_type(q) == RT_PRIM_BOX)
+            return box_boundary_t12<F>(S, bo, q, r, b1, b2) == 2 && medium_hit<F>(o, r, tmin, tmax, b1, b2, rng, t, prim);
+          if (bo.kind == RT_OBJ_PRIM) {
+            unsigned np = 0;
+            if (!prim_t_q<F>(S, q, r, -inf, inf, b1, np)) return false;
+            if (prim_type(q) <= RT_PRIM_MOVING_SPHERE && b1 == b1) return false;  // sphere_boundary_no_hit
+            return prim_t_q<F>(S, q, r, b1 + 0.0001f, inf, b2, np) && medium_hit<F>(o, r, tmin, tmax, b1, b2, rng, t, prim);
+          }
+        }
+      }
+      phase = 0;
+      target = o.a;
+      lo = -inf;
+      hi = inf;
   }
-  if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {  // constant_medium.h:34-70 (one RNG draw per qualifying query, H8)
-      float t1, t2;
-      if (!medium_boundary<F>(S, o, r, t1, t2, nnode, nprim, nfall)) return false;
-      if (t1 < tmin) t1 = tmin;
-      if (t2 > tmax) t2 = tmax;
-      if (t1 >= t2) return false;
-      if (t1 < 0) t1 = 0;
-      const float len = __builtin_sqrtf(len2(r.d));
-      const float inside = (t2 - t1) * len;
-      const float hd = o.f[0] * rtm::det_logf(rtx::uniform(rng));
-      if (hd > inside) return false;
-      t = t1 + hd / len;
-      prim = -1;
-      return true;
+  if constexpr ((F & F_BVH) == 0) {  // no traversal to share (C3): straight-line queries measured faster
+    auto leaf_q = [&](int ti, float qlo, float qhi, float& tq, int& pq) {
+      rt_object x = S.objects[ti];
+      Ray rr = r;
+      if constexpr ((F & F_XFORM) != 0) if (x.kind == RT_OBJ_XFORM) {
+          Ray moved;
+          rr = xform_ray(x, r, moved);
+          x = S.objects[x.a];
+      }
+      return leaf_closest<F>(S, x, rr, qlo, qhi, tq, pq, nnode, nprim, nfall);
+    };
+    if (phase == 2) return leaf_q(oi, tmin, tmax, t, prim);
+    float b1, b2;
+    int pq;
+    if (!leaf_q(o.a, -inf, inf, b1, pq)) return false;
+    if (sphere_boundary_no_hit<F>(S, o.a, b1)) return false;
+    if (!leaf_q(o.a, b1 + 0.0001f, inf, b2, pq)) return false;
+    return medium_hit<F>(o, r, tmin, tmax, b1, b2, rng, t, prim);
   }
-  return leaf_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall);
+  for (;;) {
+    rt_object x = S.objects[target];
+    Ray rr = r;
+    if constexpr ((F & F_XFORM) != 0) if (x.kind == RT_OBJ_XFORM) {
+        Ray moved;
+        rr = xform_ray(x, r, moved);
+        x = S.objects[x.a];
+    }
+    float tq;
+    int pq;
+    const bool hit = leaf_closest<F>(S, x, rr, lo, hi, tq, pq, nnode, nprim, nfall);
+    if (phase == 2) {
+      t = tq;
+      prim = pq;
+      return hit;
+    }
+    if (!hit) return false;
+    if (phase == 1) return medium_hit<F>(o, r, tmin, tmax, t1, tq, rng, t, prim);
+    t1 = tq;
+    if (sphere_boundary_no_hit<F>(S, o.a, t1)) return false;
+    lo = t1 + 0.0001f;
+    phase = 1;
+  }
 }
 
 template <int F>
@@ -1260,7 +1278,7 @@ struct RenderParams {
   const uint32_t* perm;
   uint16_t* item_cost;
   unsigned long long n_long;
-  uint32_t cam_state[6];
+  uint32_t cam_state[6];  // pristine slot-0 state curand_init(seed, 0, 0): REF camera draws of render_step_kernel
   // Camera-ray candidate lists (render_step_kernel; null: camera rays traverse the tree): per 8x8
   // tile of the image, tile_cnt[t] entries at tile_ent[t * tile_cap] (-1: the tile overflowed).
   const int32_t* tile_cnt;
@@ -1290,6 +1308,32 @@ constexpr int kShadeMin = 60;  // render_step_kernel: default shading-phase thre
 constexpr int kShadePasses = RT_SHADE_PASSES;  // render_step_kernel: shading passes per phase
 constexpr unsigned kChunk = 64;  // items a wave claims per work-counter atomic
 static_assert(kChunk >= 64, "claim_items: one claim must cover a refill of every lane of a wave");
+
+// Camera ray of sample s of pixel (i, j) for render_kernel (render.h:105-108, camera.h:49-58).
+// In the REF camera mode every pixel restarts a private copy of the pristine slot-0 state (H2), so
+// the lens offset and time of sample s are the same for all pixels: they come from cam_tab, built
+// on the host with the same float operations (camera_table): no camera RNG state per lane, no
+// rejection loop (C3-C5 2 % faster).  PER_PIXEL draws them from the pixel's own state, after the
+// jitter (render.h:105-108 order).
+__device__ __forceinline__ void camera_ray(const RenderParams& P, const rt_camera& C, int i, int j, int s,
+                                           bool per_pixel, Rng& loc, Ray& ray) {
+  const float u = ((float)i + rtx::uniform(loc)) / (float)P.W;
+  const float v = ((float)j + rtx::uniform(loc)) / (float)P.H;
+  V off;
+  float tm;
+  if (per_pixel) {
+    const V rd = C.lens_radius * in_unit_disk(loc);
+    off = rd.x * ld3(C.u) + rd.y * ld3(C.v);
+    tm = urange(loc, C.time0, C.time1);
+  } else {
+    const float4 e = P.S.cam_tab[s];
+    off = mk(e.x, e.y, e.z);
+    tm = e.w;
+  }
+  ray.o = ld3(C.origin) + off;
+  ray.d = ld3(C.lower_left) + u * ld3(C.horizontal) + v * ld3(C.vertical) - ld3(C.origin) - off;
+  ray.tm = tm;
+}
 
 __device__ __forceinline__ unsigned lane_rank(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
@@ -1356,7 +1400,7 @@ void render_kernel(const RenderParams P) {
   long long item = -1;  // -1: idle
   bool done = false;
   int f = 0, i = 0, r = 0, j = 0, s = 0, depth = 0;
-  Rng loc{}, cam{};
+  Rng loc{};
   Ray ray{};
   V att = mk(1, 1, 1), col = mk(0, 0, 0);
   unsigned nseg = 0, nsamp = 0;
@@ -1366,7 +1410,7 @@ void render_kernel(const RenderParams P) {
   const rt_camera& C = S.cam;
   unsigned long long chunk_base = 0;  // wave-uniform: next unclaimed item of the wave's chunk
   unsigned chunk_left = 0;
-  // cold state in the LDS locker (parks<F>): 0..5 camera RNG, 6..8 sample sum, 9 fb, 10 owned row
+  // cold state in the LDS locker (parks<F>): 0..2 sample sum, 3 fb, 4 owned row
   uint32_t* const lk = locker_of<F>();
   constexpr int LB = render_block<F>();
 
@@ -1403,11 +1447,11 @@ void render_kernel(const RenderParams P) {
           depth = 0;
           item_segs = 0;
           if constexpr (parks<F>()) {
-            lk[6 * LB] = 0u;
-            lk[7 * LB] = 0u;
-            lk[8 * LB] = 0u;
-            lk[9 * LB] = (uint32_t)f;
-            lk[10 * LB] = (uint32_t)r;
+            lk[0 * LB] = 0u;
+            lk[1 * LB] = 0u;
+            lk[2 * LB] = 0u;
+            lk[3 * LB] = (uint32_t)f;
+            lk[4 * LB] = (uint32_t)r;
           } else {
             col = mk(0, 0, 0);
           }
@@ -1419,26 +1463,8 @@ void render_kernel(const RenderParams P) {
       // ---- begin a sample: jitter + camera ray (render.h:105-108, camera.h:49-58)
       if (depth == 0) {
         RT_STAMP(1);
-        if (s == 0) {
-          cam.d = P.cam_state[0];
-          for (int k = 0; k < 5; ++k) cam.v[k] = P.cam_state[1 + k];
-        } else if constexpr (parks<F>()) {
-          cam.d = lk[0];
-          for (int k = 0; k < 5; ++k) cam.v[k] = lk[(1 + k) * LB];
-        }
-        const float u = ((float)i + rtx::uniform(loc)) / (float)P.W;
-        const float v = ((float)j + rtx::uniform(loc)) / (float)P.H;
-        Rng& cr = per_pixel ? loc : cam;
-        const V rd = C.lens_radius * in_unit_disk(cr);
-        const V off = rd.x * ld3(C.u) + rd.y * ld3(C.v);
-        ray.o = ld3(C.origin) + off;
-        ray.d = ld3(C.lower_left) + u * ld3(C.horizontal) + v * ld3(C.vertical) - ld3(C.origin) - off;
-        ray.tm = urange(cr, C.time0, C.time1);
+        camera_ray(P, C, i, j, s, per_pixel, loc, ray);
         att = mk(1.0f, 1.0f, 1.0f);
-        if constexpr (parks<F>()) {
-          lk[0] = cam.d;
-          for (int k = 0; k < 5; ++k) lk[(1 + k) * LB] = cam.v[k];
-        }
       }
 
       // ---- one segment (render.h:60-77)
@@ -1486,20 +1512,20 @@ void render_kernel(const RenderParams P) {
         }
       }
       if (ended) {
-        if constexpr (parks<F>()) col = mk(__uint_as_float(lk[6 * LB]), __uint_as_float(lk[7 * LB]), __uint_as_float(lk[8 * LB]));
+        if constexpr (parks<F>()) col = mk(__uint_as_float(lk[0 * LB]), __uint_as_float(lk[1 * LB]), __uint_as_float(lk[2 * LB]));
         col = col + contrib;
         if constexpr (parks<F>()) {
-          lk[6 * LB] = __float_as_uint(col.x);
-          lk[7 * LB] = __float_as_uint(col.y);
-          lk[8 * LB] = __float_as_uint(col.z);
+          lk[0 * LB] = __float_as_uint(col.x);
+          lk[1 * LB] = __float_as_uint(col.y);
+          lk[2 * LB] = __float_as_uint(col.z);
         }
         depth = 0;
         ++nsamp;
         if (++s == P.spp) {
           const V out = (1.0f / (float)P.spp) * col;
           if constexpr (parks<F>()) {
-            f = (int)lk[9 * LB];
-            r = (int)lk[10 * LB];
+            f = (int)lk[3 * LB];
+            r = (int)lk[4 * LB];
           }
           float* dst = P.fb + 3 * (((long long)f * P.rows + r) * P.W + i);
           dst[0] = out.x;
@@ -1686,6 +1712,9 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
       RT_STAMP(1);
       if (item >= 0 && mode == 0) {
         if (depth == 0) {
+          // REF: the step kernel draws the per-sample lens offset and time from its own copy of the
+          // pristine slot-0 state instead of cam_tab (measured faster here: the table read would sit
+          // in the shading phase's dependent chain)
           if (s == 0) {
             cam.d = P.cam_state[0];
             for (int k = 0; k < 5; ++k) cam.v[k] = P.cam_state[1 + k];
@@ -1990,6 +2019,11 @@ struct rt_ctx {
   const float4* bin_sph = nullptr;
   const int32_t* bin_ids = nullptr;
   int bin_n = 0;
+  // REF camera mode: per-sample lens offset + time of the last (scene, seed, spp) (camera_table)
+  float4* cam_tab = nullptr;
+  long long cam_cap = 0;
+  long long cam_key[3] = {-1, -1, -1};
+  std::vector<float4> cam_host;  // stays alive while the upload is in flight
   int32_t* tiles = nullptr;  // [ntiles] counts, then [ntiles * kTileCap] entries
   long long tiles_cap = 0;
   long long tiles_key[3] = {-1, -1, -1};
@@ -2264,6 +2298,29 @@ int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<
   return fb;
 }
 
+// REF camera mode (H2): each pixel draws its lens offset and time from a private copy of the
+// pristine slot-0 state curand_init(seed, 0, 0), restarted per item, so sample s of every pixel
+// uses the same draws: in_unit_disk (vec3.h:136-142, left-to-right H9) scaled by lens_radius,
+// offset = rd.x u + rd.y v, time = time0 + (time1 - time0) U (camera.h:49-58).  Same float
+// operations as the device path (-ffp-contract=off on both sides), so the rays are bit-identical.
+void camera_table(const rt_camera& C, uint64_t seed, int spp, std::vector<float4>& out) {
+  rtx::State cr = rtx::seed_state(seed);
+  out.resize((size_t)spp);
+  for (int s = 0; s < spp; ++s) {
+    float a, b;
+    bool inside;
+    do {
+      a = -1.0f + (1.0f - -1.0f) * rtx::uniform(cr);
+      b = -1.0f + (1.0f - -1.0f) * rtx::uniform(cr);
+      inside = a * a + b * b + 0.0f * 0.0f < 1.0f;
+    } while (!inside);
+    const float rx = C.lens_radius * a, ry = C.lens_radius * b;
+    const float ox = rx * C.u[0] + ry * C.v[0], oy = rx * C.u[1] + ry * C.v[1], oz = rx * C.u[2] + ry * C.v[2];
+    const float tm = C.time0 + (C.time1 - C.time0) * rtx::uniform(cr);
+    out[(size_t)s] = make_float4(ox, oy, oz, tm);
+  }
+}
+
 int validate_args(rt_ctx* c, const rt_render_args* a) {
   if (!a) return fail(c, RT_ERR_ARG, "null args");
   if (a->width <= 0 || a->height <= 0 || a->spp <= 0 || a->fb_count <= 0 || a->fb_first < 0 || a->max_depth <= 0)
@@ -2350,6 +2407,7 @@ int rt_ctx_destroy(rt_ctx* c) {
   if (c->perm) (void)hipFree(c->perm);
   if (c->dbg) (void)hipFree(c->dbg);
   if (c->tiles) (void)hipFree(c->tiles);
+  if (c->cam_tab) (void)hipFree(c->cam_tab);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2590,10 +2648,41 @@ int rt_render_init(rt_ctx* c, int32_t width, int32_t height, uint64_t seed) {
   return RT_OK;
 }
 
-int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* counters) {
+namespace {
+// A pointer the GPU kernels may write directly: device (or managed) memory.  Host memory, pinned
+// or pageable, is staged through a temporary device buffer by rt_render / rt_resolve.
+bool device_ptr(const void* p) {
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged || at.isManaged;
+}
+int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* counters);
+}  // namespace
+
+int rt_render(rt_ctx* c, const rt_render_args* a, float* fb, rt_counters* counters) {
   if (!c) return RT_ERR_ARG;
   int rc = validate_args(c, a);
   if (rc) return rc;
+  if (!fb) return fail(c, RT_ERR_ARG, "null fb");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (device_ptr(fb)) return render_dev(c, a, fb, counters);
+  // host frame buffer: render into device memory, then copy the owned rows back
+  const size_t n = (size_t)a->fb_count * rt_owned_rows(a, nullptr) * a->width * 3;
+  float* tmp = nullptr;
+  HIPCHK(c, hipMalloc((void**)&tmp, n * sizeof(float)));
+  rc = render_dev(c, a, tmp, counters);
+  if (!rc && hipMemcpy(fb, tmp, n * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(c, RT_ERR_HIP, "copy frame buffer to host");
+  (void)hipFree(tmp);
+  return rc;
+}
+
+namespace {
+int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* counters) {
+  int rc = RT_OK;
   if (!c->have_scene) return fail(c, RT_ERR_STATE, "no scene uploaded");
   if (!c->states || c->states_n != (long long)a->width * a->height || c->states_seed != a->seed)
     return fail(c, RT_ERR_STATE, "rt_render_init not called for this size/seed");
@@ -2672,6 +2761,23 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
   const rtx::State cs = rtx::seed_state(a->seed);  // pristine slot 0 = curand_init(seed, 0, 0)
   P.cam_state[0] = cs.d;
   for (int k = 0; k < 5; ++k) P.cam_state[1 + k] = cs.v[k];
+  if (a->cam_mode == RT_CAM_REF_SLOT0) {
+    const long long ckey[3] = {c->scene_gen, (long long)a->seed, a->spp};
+    if (!std::equal(ckey, ckey + 3, c->cam_key)) {
+      if (a->spp > c->cam_cap) {
+        if (c->cam_tab) HIPCHK(c, hipFree(c->cam_tab));
+        c->cam_tab = nullptr;
+        c->cam_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->cam_tab, (size_t)a->spp * sizeof(float4)));
+        c->cam_cap = a->spp;
+      }
+      camera_table(c->scene.cam, a->seed, a->spp, c->cam_host);
+      HIPCHK(c, hipMemcpyAsync(c->cam_tab, c->cam_host.data(), (size_t)a->spp * sizeof(float4), hipMemcpyHostToDevice,
+                               c->stream));
+      std::copy(ckey, ckey + 3, c->cam_key);
+    }
+    P.S.cam_tab = c->cam_tab;
+  }
 
   const bool stats = a->stats != 0;
   const bool check = (a->flags & RT_FLAG_AUDIT) != 0;
@@ -2730,7 +2836,14 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
     P.tile_mask = (const uint32_t*)c->tiles;
     P.tiles_x = tx;
   }
-  if (cull && (vm & F_STEP) != 0 && c->bin_n > 0) {
+  // Camera-ray candidate lists pay when lanes get many items each; for a small share (a rank of a
+  // multi-GPU image) the launch ends with its longest items and the lists made that tail longer
+  // (C2, one GPU rendering each rank's share: N = 4 (9.2 items per resident lane) 5.24 ms with
+  // lists vs 5.94 without, N = 8 (4.6 per lane) 4.03 vs 3.51 ms).
+  double bins_min = 6.0;  // items per resident lane
+  if (const char* e = getenv("RT_BINS_MIN_ITEMS_PER_LANE")) bins_min = atof(e);  // tuning
+  const double lanes = (double)c->cus * std::max(1, c->blocks_per_cu[var]) * bs;
+  if (cull && (vm & F_STEP) != 0 && c->bin_n > 0 && (double)P.total_items >= bins_min * lanes) {
     const long long tkey[3] = {c->scene_gen, a->width, a->height};
     if (!std::equal(tkey, tkey + 3, c->tiles_key)) {
       if (nt * (kTileCap + 1) > c->tiles_cap) {
@@ -2890,6 +3003,7 @@ int rt_render(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* co
     return fail(c, RT_ERR_HIP, "render kernel did not complete every sample");
   return RT_OK;
 }
+}  // namespace
 
 float rt_last_render_ms(const rt_ctx* c) { return c ? c->last_ms : 0.0f; }
 const char* rt_last_render_kernel(const rt_ctx* c) { return c ? c->last_kernel : ""; }
@@ -2920,19 +3034,35 @@ int rt_audit_log(rt_ctx* c, float* out, int32_t cap) {
   return (int)n;
 }
 
-int rt_resolve(rt_ctx* c, const rt_render_args* a, const float* fb_dev, uint8_t* out_dev) {
+int rt_resolve(rt_ctx* c, const rt_render_args* a, const float* fb, uint8_t* out) {
   if (!c) return RT_ERR_ARG;
   int rc = validate_args(c, a);
   if (rc) return rc;
-  if (!fb_dev || !out_dev) return fail(c, RT_ERR_ARG, "null buffer");
+  if (!fb || !out) return fail(c, RT_ERR_ARG, "null buffer");
   HIPCHK(c, hipSetDevice(c->device));
   const long long per_fb = (long long)rt_owned_rows(a, nullptr) * a->width * 3;
   const long long blocks = (per_fb + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, fb_dev, out_dev, per_fb,
-                     a->fb_count);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  return RT_OK;
+  // host buffers (either side) are staged through device memory
+  const bool fb_host = !device_ptr(fb), out_host = !device_ptr(out);
+  float* fb_tmp = nullptr;
+  uint8_t* out_tmp = nullptr;
+  if (fb_host) {
+    HIPCHK(c, hipMalloc((void**)&fb_tmp, (size_t)per_fb * a->fb_count * sizeof(float)));
+    if (hipMemcpy(fb_tmp, fb, (size_t)per_fb * a->fb_count * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+      rc = fail(c, RT_ERR_HIP, "copy frame buffer to device");
+  }
+  if (!rc && out_host && hipMalloc((void**)&out_tmp, (size_t)per_fb) != hipSuccess) rc = fail(c, RT_ERR_NOMEM, "hipMalloc out");
+  if (!rc) {
+    hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, fb_host ? fb_tmp : fb,
+                       out_host ? out_tmp : out, per_fb, a->fb_count);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)
+      rc = fail(c, RT_ERR_HIP, "resolve kernel");
+  }
+  if (!rc && out_host && hipMemcpy(out, out_tmp, (size_t)per_fb, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(c, RT_ERR_HIP, "copy image to host");
+  if (fb_tmp) (void)hipFree(fb_tmp);
+  if (out_tmp) (void)hipFree(out_tmp);
+  return rc;
 }
 
 int rt_draw(rt_ctx* c, const rt_render_args* a, uint8_t* png_rgb_host, rt_counters* counters) {

@@ -2,7 +2,10 @@
 
 For N in 1, 2, 4, 8 and every rank r < N, times rank r's step pieces as bench.py runs them
 (render_init, the render of its 4-row bands, resolve) with HIP events; the N-GPU step is bounded
-below by max over ranks (the gather and barrier are not modelled).
+below by max over ranks.  "cold" is a rank's first launch of its configuration (no longest-first
+item schedule yet: the reference's single draw()), "warm" the best of the next two.  The gather
+is modelled from its bytes (N x the largest share's 8-bit rows) at XGMI_GBS (default 64 GB/s,
+a conservative all-gather rate for a few MB over xGMI) plus 30 us of collective latency.
 
 usage: diag_scale.py [scene W H spp nfb]
 """
@@ -30,12 +33,16 @@ def timed(fn):
 
 
 t_init = min(timed(lambda: ctx.render_init(W, H, 1984)) for _ in range(3))
+xgmi = float(os.environ.get("XGMI_GBS", "64"))
 base = None
 for n in (1, 2, 4, 8):
     worst = 0.0
+    worst_cold = 0.0
     segs = 0
+    share_rows = 0
     for r in range(n):
-        args = rt.make_args(W, H, spp, 0, nfb, 50, 0, band_rows=4, band_first=r, band_stride=n)
+        args = rt.make_args(W, H, spp, 0, nfb, 50, 0, band_rows=4, band_first=r, band_stride=n,
+                            bins=os.environ.get("DIAG_BINS", "1") != "0")
         rows = rt.owned_rows(args)
         fb = torch.empty(nfb * len(rows) * W * 3, dtype=torch.float32, device="cuda")
         img = torch.empty(len(rows) * W * 3, dtype=torch.uint8, device="cuda")
@@ -45,11 +52,17 @@ for n in (1, 2, 4, 8):
             ms.append(ctx.last_render_ms())
         t_res = timed(lambda: ctx.resolve(args, fb.data_ptr(), img.data_ptr()))
         worst = max(worst, min(ms[1:]) + t_res)
+        worst_cold = max(worst_cold, ms[0] + t_res)
+        share_rows = max(share_rows, len(rows))
         segs += c["segments"]
         if os.environ.get("VERBOSE"):
-            print(f"   N={n} rank {r}: {min(ms[1:]):.2f} ms, {c['segments']} segments, "
+            print(f"   N={n} rank {r}: warm {min(ms[1:]):.2f} ms, cold {ms[0]:.2f} ms, {c['segments']} segments, "
                   f"{c['segments'] / min(ms[1:]) / 1e3:.0f} Mrays/s", flush=True)
-    step = worst + t_init
+    gbytes = n * share_rows * W * 3 if n > 1 else 0
+    t_gather = (gbytes / (xgmi * 1e6) + 0.03) if n > 1 else 0.0
+    step = worst + t_init + t_gather
+    cold = worst_cold + t_init + t_gather
     base = base or step
-    print(f"N={n}: max rank render+resolve {worst:.2f} ms + init {t_init:.2f} ms = {step:.2f} ms/step, "
-          f"{segs / step / 1e3:.0f} Mrays/s, x{base / step:.2f}", flush=True)
+    print(f"N={n}: max rank render+resolve warm {worst:.2f} / cold {worst_cold:.2f} ms + init {t_init:.2f} ms "
+          f"+ gather {t_gather:.3f} ms ({gbytes} B) = warm {step:.2f} / cold {cold:.2f} ms/step, "
+          f"{segs / step / 1e3:.0f} Mrays/s, x{base / step:.2f} (cold x{base / cold:.2f})", flush=True)

@@ -11,6 +11,10 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
+    # The product uses camera-ray tile lists only for shares with >= 6 items per resident lane
+    # (rt_render); the parity tests' small images would never reach them, so the tests force them
+    # on (test_camera_lists_on_and_off covers the default threshold).
+    os.environ.setdefault("RT_BINS_MIN_ITEMS_PER_LANE", "0")
 
 
 @pytest.fixture(scope="session")

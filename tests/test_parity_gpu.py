@@ -414,3 +414,42 @@ def test_bench_two_ranks_match_one(tmp_path):
     assert two.returncode == 0, two.stderr[-2000:]
     assert '"n_gpus": 2' in two.stdout
     assert (tmp_path / "n1.png").read_bytes() == (tmp_path / "n2.png").read_bytes()
+
+
+def test_host_buffers_match_device(rtlib, gpu_ctx, oracle):
+    """rt_render / rt_resolve also take host pointers (host or device frame buffer):
+    the kernels write a staged device buffer that is copied back; bits equal the device path's
+    and the oracle's."""
+    import torch
+
+    W, H, spp, nfb = 64, 36, 2, 2
+    dev, rows, cnt, args, fb = _gpu_render(rtlib, gpu_ctx, "big1", W, H, spp, 0, nfb, REF, band=(4, 1, 3))
+    host = np.zeros(nfb * len(rows) * W * 3, np.float32)
+    cnt_h = gpu_ctx.render(args, host.ctypes.data)
+    assert cnt_h["segments"] == cnt["segments"]
+    assert np.array_equal(_bits(host.reshape(dev.shape)), _bits(dev))
+    ref = oracle.RefScene("big1")
+    for f in range(nfb):
+        want = ref.render(W, H, spp, f, 50, REF)[0].reshape(H, W, 3)[rows]
+        assert np.array_equal(_bits(dev[f]), _bits(want))
+    out_dev = torch.zeros(len(rows) * W * 3, dtype=torch.uint8, device="cuda")
+    gpu_ctx.resolve(args, fb.data_ptr(), out_dev.data_ptr())
+    out_host = np.zeros(len(rows) * W * 3, np.uint8)
+    gpu_ctx.resolve(args, host.ctypes.data, out_host.ctypes.data)  # host in, host out
+    assert np.array_equal(out_host, out_dev.cpu().numpy())
+
+
+@pytest.mark.parametrize("threshold", ["0", "6", "1e9"], ids=["lists", "default", "traverse"])
+def test_camera_lists_on_and_off(rtlib, gpu_ctx, oracle, threshold, monkeypatch):
+    """Camera rays through the 8x8-tile candidate lists (threshold 0), the product's default
+    threshold (6 items per resident lane: off for this size) and never: same bits as the oracle."""
+    monkeypatch.setenv("RT_BINS_MIN_ITEMS_PER_LANE", threshold)
+    W, H, spp, nfb = 96, 54, 2, 2
+    gpu, rows, cnt, _, _ = _gpu_render(rtlib, gpu_ctx, "big1", W, H, spp, 0, nfb, REF)
+    ref = oracle.RefScene("big1")
+    segs = 0
+    for f in range(nfb):
+        want, c, _ = ref.render(W, H, spp, f, 50, REF)
+        segs += c["segments"]
+        assert np.array_equal(_bits(gpu[f]), _bits(want.reshape(H, W, 3)))
+    assert cnt["segments"] == segs
