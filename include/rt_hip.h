@@ -176,6 +176,8 @@ enum rt_cam_mode {
                                      schedule from the previous launch; same pixels)            */
 #define RT_FLAG_NO_CAMERA_BINS 64 /* camera rays traverse the BVH instead of testing their 8x8
                                      tile's candidate list (world = one BVH; same pixels)       */
+#define RT_FLAG_NO_SPLIT 128      /* never split the samples of the longest items over work items
+                                     on warm launches (stepwise kernel; same pixels)            */
 
 typedef struct rt_render_args {
   int32_t width, height;  /* full image size; N = width*height drives the RNG slots (H3)  */

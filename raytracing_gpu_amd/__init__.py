@@ -35,6 +35,7 @@ RT_FLAG_WIDEST = 8
 RT_FLAG_NO_STEP = 16
 RT_FLAG_NO_SCHEDULE = 32
 RT_FLAG_NO_CAMERA_BINS = 64
+RT_FLAG_NO_SPLIT = 128
 
 PRIM_SPHERE, PRIM_MOVING_SPHERE, PRIM_RECT_XY, PRIM_RECT_XZ, PRIM_RECT_YZ, PRIM_TRIANGLE = range(6)
 OBJ_PRIM, OBJ_LIST, OBJ_BVH, OBJ_XFORM, OBJ_MEDIUM = range(5)
@@ -249,12 +250,13 @@ def make_args(width: int, height: int, spp: int, fb_first: int = 0, fb_count: in
               cam_mode: int = RT_CAM_REF_SLOT0, band_rows: int = 0, band_first: int = 0, band_stride: int = 1,
               stats: bool = False, seed: int = 1984, exact: bool = False, audit: bool = False,
               lds: bool = True, widest: bool = False, step: bool = True, schedule: bool = True,
-              bins: bool = True) -> rt_render_args:
+              bins: bool = True, split: bool = True) -> rt_render_args:
     flags = (RT_FLAG_EXACT_TRAVERSAL if exact else 0) | (RT_FLAG_AUDIT if audit else 0) | (0 if lds else RT_FLAG_NO_LDS)
     flags |= RT_FLAG_WIDEST if widest else 0
     flags |= 0 if step else RT_FLAG_NO_STEP
     flags |= 0 if schedule else RT_FLAG_NO_SCHEDULE
     flags |= 0 if bins else RT_FLAG_NO_CAMERA_BINS
+    flags |= 0 if split else RT_FLAG_NO_SPLIT
     return rt_render_args(width, height, spp, fb_first, fb_count, max_depth, cam_mode,
                           band_rows if band_rows > 0 else height, band_first, band_stride,
                           1 if stats else 0, flags, seed)

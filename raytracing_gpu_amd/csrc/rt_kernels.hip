@@ -1279,6 +1279,18 @@ struct RenderParams {
   uint16_t* item_cost;
   unsigned long long n_long;
   uint32_t cam_state[6];  // pristine slot-0 state curand_init(seed, 0, 0): REF camera draws of render_step_kernel
+  // Split samples (render_step_kernel, warm launches of a small share; see rt_render): the first
+  // n_split positions of perm are the longest items.  split_mode 1: those items record their RNG
+  // state at every sample start into ckpt[pos * spp + s]; split_mode 2: their samples are separate
+  // work items (claim k < n_split * spp: position k / spp, sample k % spp) that start from ckpt
+  // (sample 0: from states) and write the sample's sum to contrib[3 k]; merge_split_kernel adds
+  // them up in sample order.  cam_st[s]: the REF camera state at sample s's start.
+  int split_mode;
+  int pad5;
+  unsigned long long n_split;
+  uint4* ckpt;
+  float* contrib;
+  const uint4* cam_st;
   // Camera-ray candidate lists (render_step_kernel; null: camera rays traverse the tree): per 8x8
   // tile of the image, tile_cnt[t] entries at tile_ent[t * tile_cap] (-1: the tile overflowed).
   const int32_t* tile_cnt;
@@ -1611,6 +1623,9 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
   unsigned long long chunk_base = 0;  // wave-uniform: next unclaimed item of the wave's chunk
   unsigned chunk_left = 0;
   bool lng = false;  // the lane's item is one of the longest of the previous launch (perm prefix)
+  int s_end = 0;     // the lane's item ends after sample s_end - 1 (spp, or one sample of a split item)
+  int ck = -1;       // split_mode 1: perm position whose sample-start states are recorded; 2: split sample
+  bool fresh = false;  // the item's first sample is next (camera state from its start)
 #ifdef RT_WAVE_TIMES
   unsigned long long wt0, wt1 = 0;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wt0)::"memory");
@@ -1655,12 +1670,19 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
           col = col + contrib;
           depth = 0;
           ++nsamp;
-          if (++s == P.spp) {
-            const V out = (1.0f / (float)P.spp) * col;
-            float* dst = P.fb + 3 * (((long long)f * P.rows + r) * P.W + i);
-            dst[0] = out.x;
-            dst[1] = out.y;
-            dst[2] = out.z;
+          if (++s == s_end) {
+            if (P.split_mode == 2 && ck >= 0) {  // one sample of a split item: its sum, merged later
+              float* dst = P.contrib + 3 * (long long)ck;
+              dst[0] = col.x;
+              dst[1] = col.y;
+              dst[2] = col.z;
+            } else {
+              const V out = (1.0f / (float)P.spp) * col;
+              float* dst = P.fb + 3 * (((long long)f * P.rows + r) * P.W + i);
+              dst[0] = out.x;
+              dst[1] = out.y;
+              dst[2] = out.z;
+            }
             if (P.row_cost && (i & 15) == 0) atomicAdd(&P.row_cost[j], (unsigned long long)item_segs);
             if (P.item_cost) P.item_cost[item] = (uint16_t)(item_segs < 65535u ? item_segs : 65535u);
             item = -1;
@@ -1681,8 +1703,23 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
             if (wt1 == 0) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wt1)::"memory");
 #endif
           } else {
-            item = P.perm ? (long long)P.perm[mine] : (long long)mine;
-            lng = mine < P.n_long;
+            unsigned long long pos = mine;
+            int sa = 0;
+            ck = -1;
+            if (P.split_mode == 2) {  // split samples first, then the rest of perm
+              const unsigned long long nsub = P.n_split * (unsigned long long)P.spp;
+              if (mine < nsub) {
+                pos = mine / (unsigned)P.spp;
+                sa = (int)(mine - pos * (unsigned)P.spp);
+                ck = (int)mine;
+              } else {
+                pos = mine - nsub + P.n_split;
+              }
+            } else if (P.split_mode == 1 && mine < P.n_split) {
+              ck = (int)mine;
+            }
+            item = P.perm ? (long long)P.perm[pos] : (long long)pos;
+            lng = pos < P.n_long;
             const long long per_row = (long long)P.fb_count * P.W;  // same item order as render_kernel
             const int q = (int)(item / per_row);
             const long long rem = item - (long long)q * per_row;
@@ -1693,9 +1730,12 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
             const long long id = P.fb_first + f;
             const long long p = (long long)j * P.W + i;
             const long long slot = ((id + 1) * p + id + 1) % P.npix;  // render.h:101 (H3)
-            const uint4 s0 = P.states[2 * slot], s1 = P.states[2 * slot + 1];
+            const uint4* st = sa > 0 ? P.ckpt + 2 * (long long)mine : P.states + 2 * slot;
+            const uint4 s0 = st[0], s1 = st[1];
             loc.d = s0.x; loc.v[0] = s0.y; loc.v[1] = s0.z; loc.v[2] = s0.w; loc.v[3] = s1.x; loc.v[4] = s1.y;
-            s = 0;
+            s = sa;
+            s_end = (P.split_mode == 2 && ck >= 0) ? sa + 1 : P.spp;
+            fresh = true;
             depth = 0;
             item_segs = 0;
             col = mk(0, 0, 0);
@@ -1715,9 +1755,20 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
           // REF: the step kernel draws the per-sample lens offset and time from its own copy of the
           // pristine slot-0 state instead of cam_tab (measured faster here: the table read would sit
           // in the shading phase's dependent chain)
-          if (s == 0) {
-            cam.d = P.cam_state[0];
-            for (int k = 0; k < 5; ++k) cam.v[k] = P.cam_state[1 + k];
+          if (fresh && !per_pixel) {
+            if (s == 0) {
+              cam.d = P.cam_state[0];
+              for (int k = 0; k < 5; ++k) cam.v[k] = P.cam_state[1 + k];
+            } else {  // a split sample: the camera state at its start
+              const uint4 c0 = P.cam_st[2 * s], c1 = P.cam_st[2 * s + 1];
+              cam.d = c0.x; cam.v[0] = c0.y; cam.v[1] = c0.z; cam.v[2] = c0.w; cam.v[3] = c1.x; cam.v[4] = c1.y;
+            }
+          }
+          fresh = false;
+          if (P.split_mode == 1 && ck >= 0 && s > 0) {  // record the sample-start state for split launches
+            uint4* dst = P.ckpt + 2 * ((long long)ck * P.spp + s);
+            dst[0] = make_uint4(loc.d, loc.v[0], loc.v[1], loc.v[2]);
+            dst[1] = make_uint4(loc.v[3], loc.v[4], 0u, 0u);
           }
           const float u = ((float)i + rtx::uniform(loc)) / (float)P.W;
           const float v = ((float)j + rtx::uniform(loc)) / (float)P.H;
@@ -1879,6 +1930,29 @@ __global__ __launch_bounds__(kBlock) void resolve_kernel(const float* __restrict
   out[k] = (uint8_t)quant(acc / (float)nfb);
 }
 
+// Split items (render_step_kernel split_mode 2): the fb value of each of the first n_split items
+// of perm from its samples' sums, added in sample order from 0 -- the same float additions as the
+// item's own loop (col = 0; col += sample sum; (0 + x) + y == x + y for every x that is not -0,
+// and a sample sum 0 + c is never -0) -- then scaled by 1 / spp as render.h:111 does.
+__global__ __launch_bounds__(kBlock) void merge_split_kernel(const RenderParams P) {
+  const long long p = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (p >= (long long)P.n_split) return;
+  const long long item = P.perm[p];
+  const long long per_row = (long long)P.fb_count * P.W;
+  const int q = (int)(item / per_row);
+  const long long rem = item - (long long)q * per_row;
+  const int r = P.row_order[q];
+  const int f = (int)(rem / P.W);
+  const int i = (int)(rem - (long long)f * P.W);
+  V col = mk(0.0f, 0.0f, 0.0f);
+  for (int s = 0; s < P.spp; ++s) col = col + ld3(P.contrib + 3 * (p * P.spp + s));
+  const V out = (1.0f / (float)P.spp) * col;
+  float* dst = P.fb + 3 * (((long long)f * P.rows + r) * P.W + i);
+  dst[0] = out.x;
+  dst[1] = out.y;
+  dst[2] = out.z;
+}
+
 // Camera-ray culling per 8x8-pixel tile.  A camera ray (render.h:105-108, camera.h:49-58) is
 //   X(t) = O + off + t (F - O - off),  F = lower_left + u horizontal + v vertical,
 // with (u, v) inside the tile (jitter in [0, 1] of a pixel), |off| <= lens_radius = L and its time
@@ -2006,6 +2080,18 @@ struct rt_ctx {
   long long item_cap = 0;
   long long perm_key[10] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
   unsigned long long n_long = 0;
+  // Split samples of the longest items (render_step_kernel; see rt_render): n_split perm positions,
+  // split_state 0 = record on the next launch of perm_key, 1 = recorded for split_seed.
+  unsigned long long n_split = 0;
+  int split_state = -1;
+  uint64_t split_seed = 0;
+  uint4* ckpt = nullptr;
+  long long ckpt_cap = 0;  // uint4 pairs
+  float* contrib = nullptr;
+  long long contrib_cap = 0;  // floats
+  uint4* cam_st = nullptr;
+  long long cam_st_cap = 0;  // uint4 pairs
+  long long cam_st_key[3] = {-1, -1, -1};
   long long scene_gen = 0;
   int cus = 0, blocks_per_cu[32] = {0};  // per kernel variant (kVariants)
   int features = 0;
@@ -2024,6 +2110,7 @@ struct rt_ctx {
   long long cam_cap = 0;
   long long cam_key[3] = {-1, -1, -1};
   std::vector<float4> cam_host;  // stays alive while the upload is in flight
+  std::vector<uint4> cam_st_host;
   int32_t* tiles = nullptr;  // [ntiles] counts, then [ntiles * kTileCap] entries
   long long tiles_cap = 0;
   long long tiles_key[3] = {-1, -1, -1};
@@ -2303,10 +2390,18 @@ int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<
 // uses the same draws: in_unit_disk (vec3.h:136-142, left-to-right H9) scaled by lens_radius,
 // offset = rd.x u + rd.y v, time = time0 + (time1 - time0) U (camera.h:49-58).  Same float
 // operations as the device path (-ffp-contract=off on both sides), so the rays are bit-identical.
-void camera_table(const rt_camera& C, uint64_t seed, int spp, std::vector<float4>& out) {
+// states (optional): the camera RNG state at each sample's start, 2 uint4 per sample as the
+// step kernel loads them (d v0 v1 v2 | v3 v4 - -).
+void camera_table(const rt_camera& C, uint64_t seed, int spp, std::vector<float4>& out,
+                  std::vector<uint4>* states = nullptr) {
   rtx::State cr = rtx::seed_state(seed);
   out.resize((size_t)spp);
+  if (states) states->resize(2 * (size_t)spp);
   for (int s = 0; s < spp; ++s) {
+    if (states) {
+      (*states)[2 * (size_t)s] = make_uint4(cr.d, cr.v[0], cr.v[1], cr.v[2]);
+      (*states)[2 * (size_t)s + 1] = make_uint4(cr.v[3], cr.v[4], 0u, 0u);
+    }
     float a, b;
     bool inside;
     do {
@@ -2408,6 +2503,9 @@ int rt_ctx_destroy(rt_ctx* c) {
   if (c->dbg) (void)hipFree(c->dbg);
   if (c->tiles) (void)hipFree(c->tiles);
   if (c->cam_tab) (void)hipFree(c->cam_tab);
+  if (c->ckpt) (void)hipFree(c->ckpt);
+  if (c->contrib) (void)hipFree(c->contrib);
+  if (c->cam_st) (void)hipFree(c->cam_st);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2792,6 +2890,54 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   P.shade_min = kShadeMin;
   P.perm = have_perm ? c->perm : nullptr;
   P.n_long = have_perm ? c->n_long : 0;
+  // Split samples of the longest items (stepwise kernel; scheduled launches of a configuration
+  // with split items): the launch after the measuring one records their sample-start RNG states,
+  // later launches with the same seed run each of their samples as a separate work item.
+  const bool split_ok = have_perm && c->n_split > 0 && (kVariants[var].mask & F_STEP) != 0 && a->spp > 1 &&
+                        (a->flags & RT_FLAG_NO_SPLIT) == 0;
+  int split_mode = 0;
+  if (split_ok && c->split_state == 1 && c->split_seed == a->seed) split_mode = 2;
+  else if (split_ok) split_mode = 1;
+  if (split_mode != 0) {
+    const long long need = (long long)c->n_split * a->spp;
+    if (need > c->ckpt_cap) {
+      if (c->ckpt) HIPCHK(c, hipFree(c->ckpt));
+      c->ckpt = nullptr;
+      c->ckpt_cap = 0;
+      c->split_state = -1;
+      HIPCHK(c, hipMalloc((void**)&c->ckpt, (size_t)need * 2 * sizeof(uint4)));
+      c->ckpt_cap = need;
+      split_mode = 1;
+    }
+    if (split_mode == 2 && 3 * need > c->contrib_cap) {
+      if (c->contrib) HIPCHK(c, hipFree(c->contrib));
+      c->contrib = nullptr;
+      c->contrib_cap = 0;
+      HIPCHK(c, hipMalloc((void**)&c->contrib, (size_t)need * 3 * sizeof(float)));
+      c->contrib_cap = 3 * need;
+    }
+    const long long skey[3] = {c->scene_gen, (long long)a->seed, a->spp};
+    if (!std::equal(skey, skey + 3, c->cam_st_key)) {  // REF camera state at every sample start
+      if (a->spp > c->cam_st_cap) {
+        if (c->cam_st) HIPCHK(c, hipFree(c->cam_st));
+        c->cam_st = nullptr;
+        c->cam_st_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->cam_st, (size_t)a->spp * 2 * sizeof(uint4)));
+        c->cam_st_cap = a->spp;
+      }
+      std::vector<float4> unused;
+      camera_table(c->scene.cam, a->seed, a->spp, unused, &c->cam_st_host);
+      HIPCHK(c, hipMemcpyAsync(c->cam_st, c->cam_st_host.data(), c->cam_st_host.size() * sizeof(uint4),
+                               hipMemcpyHostToDevice, c->stream));
+      std::copy(skey, skey + 3, c->cam_st_key);
+    }
+    P.split_mode = split_mode;
+    P.n_split = c->n_split;
+    P.ckpt = c->ckpt;
+    P.contrib = c->contrib;
+    P.cam_st = c->cam_st;
+    if (split_mode == 2) P.total_items = (unsigned long long)need + (unsigned long long)(items - (long long)c->n_split);
+  }
   P.item_cost = (sched && !have_perm) ? c->item_cost : nullptr;
   if (const char* e = getenv("RT_SHADE_MIN")) P.shade_min = std::max(1, std::min(64, atoi(e)));
   if (check) {
@@ -2902,6 +3048,10 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   void* kargs[] = {&P};
   HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), kargs, shmem, c->stream));
   HIPCHK(c, hipGetLastError());
+  if (split_mode == 2) {
+    merge_split_kernel<<<(unsigned)((c->n_split + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(P);
+    HIPCHK(c, hipGetLastError());
+  }
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   snprintf(c->last_kernel, sizeof(c->last_kernel), "%s<%d>",
            (kVariants[var].mask & F_STEP) != 0 ? "render_step_kernel" : "render_kernel", kVariants[var].mask);
@@ -2952,7 +3102,25 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     HIPCHK(c, hipMemcpyAsync(c->perm, pm.data(), pm.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->n_long = (unsigned long long)nl;
+    // Items longer than half a resident lane's share of this launch's segments (at least 32) can
+    // decide when a small share ends: their samples are split on later launches.  They are the
+    // first positions of perm (cost buckets descending).
+    {
+      const double lanes = (double)c->cus * std::max(1, c->blocks_per_cu[var]) * bs;
+      double thr = std::max(32.0, 0.5 * (double)host_cnt[1] / lanes);
+      if (const char* e = getenv("RT_SPLIT_MIN_SEGMENTS")) thr = atof(e);  // tuning
+      const long long bt = (long long)std::ceil(thr / (double)(1 << shift));
+      long long ns = 0;
+      for (long long v = 65535; v >= bt && v >= 0; --v) ns += hist[(size_t)v];
+      if (ns * (long long)a->spp >= (1LL << 30)) ns = 0;
+      c->n_split = (unsigned long long)ns;
+      c->split_state = ns > 0 ? 0 : -1;
+    }
     std::copy(pkey, pkey + 10, c->perm_key);
+  }
+  if (split_mode == 1) {  // sample-start states recorded for this seed
+    c->split_state = 1;
+    c->split_seed = a->seed;
   }
   HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
   if (counters) {
@@ -2999,7 +3167,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     fclose(fo);
   }
 #endif
-  if (host_cnt[4] != (unsigned long long)a->spp * P.total_items)
+  if (host_cnt[4] != (unsigned long long)a->spp * (unsigned long long)items)  // split samples: items != work items
     return fail(c, RT_ERR_HIP, "render kernel did not complete every sample");
   return RT_OK;
 }

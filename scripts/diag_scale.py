@@ -3,7 +3,7 @@
 For N in 1, 2, 4, 8 and every rank r < N, times rank r's step pieces as bench.py runs them
 (render_init, the render of its 4-row bands, resolve) with HIP events; the N-GPU step is bounded
 below by max over ranks.  "cold" is a rank's first launch of its configuration (no longest-first
-item schedule yet: the reference's single draw()), "warm" the best of the next two.  The gather
+item schedule yet: the reference's single draw()), "warm" the best of launches 3 and 4 (launch 2 records the split items' sample-start states).  The gather
 is modelled from its bytes (N x the largest share's 8-bit rows) at XGMI_GBS (default 64 GB/s,
 a conservative all-gather rate for a few MB over xGMI) plus 30 us of collective latency.
 
@@ -47,17 +47,17 @@ for n in (1, 2, 4, 8):
         fb = torch.empty(nfb * len(rows) * W * 3, dtype=torch.float32, device="cuda")
         img = torch.empty(len(rows) * W * 3, dtype=torch.uint8, device="cuda")
         ms = []
-        for _ in range(3):  # the first launch of a configuration measures the row costs
+        for _ in range(4):  # launch 1 measures the item costs, 2 records split states, 3+ are warm
             c = ctx.render(args, fb.data_ptr())
             ms.append(ctx.last_render_ms())
         t_res = timed(lambda: ctx.resolve(args, fb.data_ptr(), img.data_ptr()))
-        worst = max(worst, min(ms[1:]) + t_res)
+        worst = max(worst, min(ms[2:]) + t_res)
         worst_cold = max(worst_cold, ms[0] + t_res)
         share_rows = max(share_rows, len(rows))
         segs += c["segments"]
         if os.environ.get("VERBOSE"):
-            print(f"   N={n} rank {r}: warm {min(ms[1:]):.2f} ms, cold {ms[0]:.2f} ms, {c['segments']} segments, "
-                  f"{c['segments'] / min(ms[1:]) / 1e3:.0f} Mrays/s", flush=True)
+            print(f"   N={n} rank {r}: warm {min(ms[2:]):.2f} ms, cold {ms[0]:.2f} ms, 2nd {ms[1]:.2f} ms, "
+                  f"{c['segments']} segments, {c['segments'] / min(ms[2:]) / 1e3:.0f} Mrays/s", flush=True)
     gbytes = n * share_rows * W * 3 if n > 1 else 0
     t_gather = (gbytes / (xgmi * 1e6) + 0.03) if n > 1 else 0.0
     step = worst + t_init + t_gather

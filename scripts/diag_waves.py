@@ -21,8 +21,8 @@ args = rt.make_args(W, H, spp, 0, nfb, 50, 0, band_rows=4, band_first=0, band_st
 rows = rt.owned_rows(args)
 fb = torch.empty(nfb * len(rows) * W * 3, dtype=torch.float32, device="cuda")
 out = "/tmp/wave_times.bin"
-for k in range(3):
-    if k == 2:
+for k in range(4):
+    if k == 3:
         os.environ["RT_WAVE_TIMES_OUT"] = out
     ctx.render(args, fb.data_ptr())
 ms = ctx.last_render_ms()

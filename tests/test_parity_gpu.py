@@ -453,3 +453,34 @@ def test_camera_lists_on_and_off(rtlib, gpu_ctx, oracle, threshold, monkeypatch)
         segs += c["segments"]
         assert np.array_equal(_bits(gpu[f]), _bits(want.reshape(H, W, 3)))
     assert cnt["segments"] == segs
+
+
+@pytest.mark.parametrize("min_segs", [None, "1"], ids=["default", "every_item"])
+@pytest.mark.parametrize("band", [None, (4, 1, 3)], ids=["full", "share"])
+def test_split_samples_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch, min_segs, band):
+    """Warm launches split the samples of the longest items over work items (launch 1 measures,
+    launch 2 records the sample-start RNG states, launches 3+ split and merge): every launch's
+    frame buffer equals the oracle's bit for bit, with the same segment and sample counts."""
+    import torch
+
+    if min_segs:
+        monkeypatch.setenv("RT_SPLIT_MIN_SEGMENTS", min_segs)
+    W, H, spp, nfb = 96, 54, 4, 2
+    sc = rtlib.Scene.builtin("big1")
+    gpu_ctx.upload(sc)  # new scene generation: a fresh schedule
+    ref = oracle.RefScene("big1")
+    want = [ref.render(W, H, spp, f, 50, REF) for f in range(nfb)]
+    kw = {} if band is None else dict(band_rows=band[0], band_first=band[1], band_stride=band[2])
+    args = rtlib.make_args(W, H, spp, 0, nfb, 50, REF, **kw)
+    rows = rtlib.owned_rows(args)
+    segs = sum(int(w[1]["segments"]) for w in want) if band is None else None
+    for launch in range(4):
+        gpu_ctx.render_init(W, H, 1984)
+        fb = torch.full((nfb * len(rows) * W * 3,), float("nan"), dtype=torch.float32, device="cuda")
+        cnt = gpu_ctx.render(args, fb.data_ptr())
+        got = fb.cpu().numpy().reshape(nfb, len(rows), W, 3)
+        for f in range(nfb):
+            assert np.array_equal(_bits(got[f]), _bits(want[f][0].reshape(H, W, 3)[rows])), f"launch {launch} fb {f}"
+        assert cnt["samples"] == nfb * len(rows) * W * spp
+        if segs is not None:
+            assert cnt["segments"] == segs
