@@ -3102,12 +3102,16 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     HIPCHK(c, hipMemcpyAsync(c->perm, pm.data(), pm.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->n_long = (unsigned long long)nl;
-    // Items longer than half a resident lane's share of this launch's segments (at least 32) can
-    // decide when a small share ends: their samples are split on later launches.  They are the
-    // first positions of perm (cost buckets descending).
+    // Items that can decide when a launch ends have their samples split on later launches: in a
+    // small share (< 6 items per resident lane, as for the camera lists) every item of >= 24
+    // segments, else items longer than half a resident lane's share of the segments (at least 32).
+    // They are the first positions of perm (cost buckets descending).  C2, one GPU per rank's
+    // share: N = 8 share 3.59 -> 2.88 ms with 24 (3.34 ms with the large-share rule, 3.15 with
+    // 12); at N = 1 and 2 a fixed 24 costs 3.5 % and 2 % (the split samples' extra claims and
+    // state loads), hence the rule by share size.
     {
       const double lanes = (double)c->cus * std::max(1, c->blocks_per_cu[var]) * bs;
-      double thr = std::max(32.0, 0.5 * (double)host_cnt[1] / lanes);
+      double thr = (double)items < 6.0 * lanes ? 24.0 : std::max(32.0, 0.5 * (double)host_cnt[1] / lanes);
       if (const char* e = getenv("RT_SPLIT_MIN_SEGMENTS")) thr = atof(e);  // tuning
       const long long bt = (long long)std::ceil(thr / (double)(1 << shift));
       long long ns = 0;
