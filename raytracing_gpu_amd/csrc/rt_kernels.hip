@@ -717,16 +717,28 @@ __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r,
 // is in the list, so the candidates of the culled search are all tested here instead of traversing
 // the tree; bvh_settle then decides the query exactly as after a traversal.
 template <int F>
-__device__ __forceinline__ void tile_candidates(const DScene& S, const int32_t* __restrict__ ent, int cnt,
+__device__ __forceinline__ void tile_candidates(const DScene& S, const int32_t* __restrict__ ent, int cnt, int4 g0,
                                                 const Ray& r, float a, float rcpa, float tmin, float tmax,
                                                 float& blo, float& bhi, float& second, int& best_prim,
                                                 int& best_rank, unsigned& nprim) {
-  for (int k = 0; k < cnt; ++k) {
-    const int pi = ent[k];
-    const PrimRec q = load_prim<F>(S, pi);
-    float lo, hi;
-    if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim))
-      take_candidate(lo, hi, pi, __float_as_int(q.c.y), blo, bhi, second, best_prim, best_rank);
+  // Entries four at a time (one 16-byte global load per group instead of one load per entry), the
+  // next group's load issued before the current group's tests.  g0 = the first group, loaded by the
+  // caller together with the count.
+  const int4* __restrict__ e4 = reinterpret_cast<const int4*>(ent);
+  int4 gn = g0;
+  for (int k = 0; k < cnt; k += 4) {
+    const int4 g = gn;
+    if (k + 4 < cnt) gn = e4[(k >> 2) + 1];
+    #pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (k + u < cnt) {
+        const int pi = u == 0 ? g.x : (u == 1 ? g.y : (u == 2 ? g.z : g.w));
+        const PrimRec q = load_prim<F>(S, pi);
+        float lo, hi;
+        if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim))
+          take_candidate(lo, hi, pi, __float_as_int(q.c.y), blo, bhi, second, best_prim, best_rank);
+      }
+    }
   }
 }
 
@@ -1798,9 +1810,11 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
         mode = 1;
         if (depth == 0 && P.tile_cnt) {  // camera ray: the tile's candidate list instead of the tree
           const int t = (j >> kTileShift) * P.tiles_x + (i >> kTileShift);
+          const int32_t* ent = P.tile_ent + (size_t)t * P.tile_cap;
           const int cnt = P.tile_cnt[t];
+          const int4 g0 = *reinterpret_cast<const int4*>(ent);  // issued with the count load
           if (cnt >= 0) {
-            tile_candidates<F>(S, P.tile_ent + (size_t)t * P.tile_cap, cnt, ray, qa, rcpa, tmin, tmax, best, bhi,
+            tile_candidates<F>(S, ent, cnt, g0, ray, qa, rcpa, tmin, tmax, best, bhi,
                                second, best_prim, best_rank, nprim);
             mode = 2;
           }
@@ -2963,7 +2977,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   const int vm = kVariants[var].mask;
   const bool cull = (a->flags & RT_FLAG_NO_CAMERA_BINS) == 0 && (vm & (F_EXACT | F_CHECK)) == 0;
   const int tx = (a->width + (1 << kTileShift) - 1) >> kTileShift, ty = (a->height + (1 << kTileShift) - 1) >> kTileShift;
-  const long long nt = (long long)tx * ty;
+  const long long nt = (long long)tx * ty, ntp = (nt + 3) & ~3LL;  // tile lists: counts, then entries from ntp
   if (cull && (vm & F_STEP) == 0 && c->bin_n < 0) {
     const long long tkey[3] = {c->scene_gen, a->width, -1 - (long long)a->height};
     if (!std::equal(tkey, tkey + 3, c->tiles_key)) {
@@ -2992,20 +3006,20 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   if (cull && (vm & F_STEP) != 0 && c->bin_n > 0 && (double)P.total_items >= bins_min * lanes) {
     const long long tkey[3] = {c->scene_gen, a->width, a->height};
     if (!std::equal(tkey, tkey + 3, c->tiles_key)) {
-      if (nt * (kTileCap + 1) > c->tiles_cap) {
+      if (ntp + nt * kTileCap > c->tiles_cap) {
         if (c->tiles) HIPCHK(c, hipFree(c->tiles));
         c->tiles = nullptr;
         c->tiles_cap = 0;
-        HIPCHK(c, hipMalloc((void**)&c->tiles, (size_t)nt * (kTileCap + 1) * sizeof(int32_t)));
-        c->tiles_cap = nt * (kTileCap + 1);
+        HIPCHK(c, hipMalloc((void**)&c->tiles, (size_t)(ntp + nt * kTileCap) * sizeof(int32_t)));
+        c->tiles_cap = ntp + nt * kTileCap;
       }
       bin_tiles_kernel<<<(unsigned)((nt + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
-          c->bin_sph, c->bin_ids, c->bin_n, c->scene.cam, a->width, a->height, tx, ty, c->tiles, c->tiles + nt);
+          c->bin_sph, c->bin_ids, c->bin_n, c->scene.cam, a->width, a->height, tx, ty, c->tiles, c->tiles + ntp);
       HIPCHK(c, hipGetLastError());
       std::copy(tkey, tkey + 3, c->tiles_key);
     }
     P.tile_cnt = c->tiles;
-    P.tile_ent = c->tiles + nt;
+    P.tile_ent = c->tiles + ntp;  // 16-byte aligned: tile_candidates reads int4 groups
     P.tiles_x = tx;
     P.tile_cap = kTileCap;
   }
