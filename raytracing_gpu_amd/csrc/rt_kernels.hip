@@ -1763,6 +1763,18 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
       // ---- next query: camera ray at a sample's start (render.h:105-108, camera.h:49-58)
       RT_STAMP(1);
       if (item >= 0 && mode == 0) {
+        // camera ray: its tile's candidate list (count + first entries) is loaded before the ray is
+        // generated, so the loads overlap the camera arithmetic
+        const bool listed = depth == 0 && P.tile_cnt != nullptr;
+        const int32_t* ent = nullptr;
+        int tcnt = -1;
+        int4 g0 = make_int4(0, 0, 0, 0);
+        if (listed) {
+          const int t = (j >> kTileShift) * P.tiles_x + (i >> kTileShift);
+          ent = P.tile_ent + (size_t)t * P.tile_cap;
+          tcnt = P.tile_cnt[t];
+          g0 = *reinterpret_cast<const int4*>(ent);
+        }
         if (depth == 0) {
           // REF: the step kernel draws the per-sample lens offset and time from its own copy of the
           // pristine slot-0 state instead of cam_tab (measured faster here: the table read would sit
@@ -1808,16 +1820,10 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
         sp = 0;
         overflow = false;
         mode = 1;
-        if (depth == 0 && P.tile_cnt) {  // camera ray: the tile's candidate list instead of the tree
-          const int t = (j >> kTileShift) * P.tiles_x + (i >> kTileShift);
-          const int32_t* ent = P.tile_ent + (size_t)t * P.tile_cap;
-          const int cnt = P.tile_cnt[t];
-          const int4 g0 = *reinterpret_cast<const int4*>(ent);  // issued with the count load
-          if (cnt >= 0) {
-            tile_candidates<F>(S, ent, cnt, g0, ray, qa, rcpa, tmin, tmax, best, bhi,
-                               second, best_prim, best_rank, nprim);
-            mode = 2;
-          }
+        if (listed && tcnt >= 0) {  // camera ray: the tile's candidate list instead of the tree
+          tile_candidates<F>(S, ent, tcnt, g0, ray, qa, rcpa, tmin, tmax, best, bhi, second, best_prim, best_rank,
+                             nprim);
+          mode = 2;
         }
       }
       if (pass + 1 >= kShadePasses || __ballot(mode == 2) == 0) break;
