@@ -1602,7 +1602,8 @@ __device__ unsigned long long rt_wave_times[3 * 8192];  // per wave: start, glob
 __device__ unsigned rt_wave_count;
 #endif
 template <int F>
-__global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const RenderParams P) {
+__global__ __launch_bounds__(render_block<F>()) __attribute__((amdgpu_waves_per_eu(render_wpe<F>())))
+void render_step_kernel(const RenderParams P) {
   const DScene& S = P.S;
   if constexpr ((F & F_LDS) != 0) stage_lds<F>(S);  // nodes, primitives, margins, materials, textures
   const unsigned lane = __lane_id();
@@ -1657,8 +1658,20 @@ __global__ __launch_bounds__(render_block<F>()) void render_step_kernel(const Re
         ++item_segs;
         bool ended = false;
         V contrib;
-        if (!bvh_settle<F>(S, obj.a, obj.b, ray, tmin, tmax, overflow, bhi, second, best, best_prim, best_rank, nnode,
-                           nprim, nfall)) {
+        bool hit = bvh_settle<F>(S, obj.a, obj.b, ray, tmin, tmax, overflow, bhi, second, best, best_prim, best_rank,
+                                 nnode, nprim, nfall);
+        // primitive objects after the BVH in the world list (C4's ground sphere): hittable_list's
+        // rule, t_max = the closest hit so far (inclusive), so a later entry wins a tie
+        for (int w = 1; w < S.n_world; ++w) {
+          const rt_object po = S.objects[S.world[w]];
+          float tq;
+          if (prim_t<F>(S, po.a, ray, tmin, hit ? best : tmax, tq, nprim)) {
+            hit = true;
+            best = tq;
+            best_prim = po.a;
+          }
+        }
+        if (!hit) {
           contrib = att * ld3(S.bg);
           ended = true;
         } else {
@@ -2115,7 +2128,8 @@ struct rt_ctx {
   long long scene_gen = 0;
   int cus = 0, blocks_per_cu[32] = {0};  // per kernel variant (kVariants)
   int features = 0;
-  bool world_bvh = false;  // the world list is one BVH object (render_step_kernel applies)
+  bool world_bvh = false;  // the world list is one BVH object (camera tile lists apply)
+  bool world_step = false;  // one BVH object followed by primitive objects (render_step_kernel applies)
   int dev_nodes = 0, dev_prims = 0, dev_mats = 0, dev_texs = 0;  // device array sizes (for LDS staging)
   float last_ms = 0.0f;
   char last_kernel[48] = "";  // rocprof name stem of the last render launch, e.g. render_step_kernel<25730>
@@ -2152,6 +2166,7 @@ const Variant kVariants[] = {
 #else
     RT_VARIANT_STEP(F_SPHERES | F_LDS | F_STEP),
     RT_VARIANT_STEP(F_SPHERES | F_STEP),
+    RT_VARIANT_STEP(F_MESH | F_STEP),
     RT_VARIANT(F_SPHERES),
     RT_VARIANT(F_ALL),
     RT_VARIANT(F_SPHERES | F_STATS),
@@ -2706,6 +2721,8 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   d.bg[2] = s->background[2];
   c->features = scene_features(s);
   c->world_bvh = s->n_world == 1 && s->objects[s->world[0]].kind == RT_OBJ_BVH;
+  c->world_step = s->n_world <= 8 && s->objects[s->world[0]].kind == RT_OBJ_BVH;
+  for (int w = 1; w < s->n_world; ++w) c->world_step = c->world_step && s->objects[s->world[w]].kind == RT_OBJ_PRIM;
   c->bin_sph = nullptr;
   c->bin_ids = nullptr;
   c->bin_n = 0;
@@ -2903,7 +2920,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
       (size_t)(2 * c->dev_nodes + 3 * c->dev_prims + (c->dev_prims + 1) / 2 + c->dev_mats + 2 * c->dev_texs) * sizeof(float4);
   const bool use_lds = lds_bytes + 1024 * kStackDepth * 2 <= (size_t)kLdsBudget && c->dev_nodes / 2 < 32768 &&
                        c->dev_prims < 32768 && (a->flags & RT_FLAG_NO_LDS) == 0;
-  const bool step = c->world_bvh && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
+  const bool step = c->world_step && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
   const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
                                (a->flags & RT_FLAG_WIDEST) != 0, step);
   // shading phase of render_step_kernel once this many lanes of a wave wait (RT_SHADE_MIN: tuning)
