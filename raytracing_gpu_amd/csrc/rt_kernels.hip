@@ -1326,6 +1326,7 @@ constexpr int kTileShift = 3;  // camera-ray candidate lists per 8x8-pixel tile
 constexpr int kTileCap = 32;   // entries per tile list (a fuller tile traverses the tree)
 constexpr int kRefill = 16;  // refill a wave once this many lanes are idle
 constexpr int kShadeMin = 60;  // render_step_kernel: default shading-phase threshold
+constexpr int kShadeMinMesh = 48;  // ... for triangle-mesh variants
 #ifndef RT_SHADE_PASSES
 #define RT_SHADE_PASSES 2
 #endif
@@ -2924,7 +2925,8 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
                                (a->flags & RT_FLAG_WIDEST) != 0, step);
   // shading phase of render_step_kernel once this many lanes of a wave wait (RT_SHADE_MIN: tuning)
-  P.shade_min = kShadeMin;
+  // (measured: C2 best at 60 of 64 lanes; C4's triangle-mesh steps at 48: 125.0 -> 119.7 ms, 40: 121.8)
+  P.shade_min = (kVariants[var].mask & F_TRI) != 0 ? kShadeMinMesh : kShadeMin;
   P.perm = have_perm ? c->perm : nullptr;
   P.n_long = have_perm ? c->n_long : 0;
   // Split samples of the longest items (stepwise kernel; scheduled launches of a configuration
