@@ -217,7 +217,9 @@ def test_band_tiles_stitch_to_full_frame(rtlib, gpu_ctx):
 
 @pytest.mark.parametrize("scene,W,H,spp,rows", [
     ("big1", 1200, 800, 2, (3, 97)),        # C2 size (1200x800), 9 rows
+    ("big1", 1200, 800, 4, (1, 40)),        # C2 size, 20 rows at 4 spp
     ("cornell_smoke", 800, 800, 2, (5, 131)),  # C3 size, 7 rows
+    ("cornell_smoke", 800, 800, 4, (2, 25)),   # C3 size, 32 rows at 4 spp
 ])
 def test_full_size_row_subset(rtlib, gpu_ctx, oracle, scene, W, H, spp, rows):
     gpu, _, _, _, _ = _gpu_render(rtlib, gpu_ctx, scene, W, H, spp, 0, 1, REF)
@@ -484,3 +486,30 @@ def test_split_samples_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch, min_segs, 
         assert cnt["samples"] == nfb * len(rows) * W * spp
         if segs is not None:
             assert cnt["segments"] == segs
+
+
+@pytest.mark.parametrize("scene,W,H,spp,rows", [
+    ("door", 1920, 1079, 2, (7, 120)),    # C4 size (1920x1079), 9 rows
+    ("final", 3840, 2159, 1, (11, 270)),  # C5 size (3840x2159), 8 rows
+])
+def test_full_size_mesh_rows(rtlib, gpu_ctx, oracle, scene, W, H, spp, rows):
+    """C4 / C5 at their full image sizes (bench.py's assets: the door mesh fixture, synthetic
+    textures of the real files' shapes), a row subset against the oracle, two fbs."""
+    import os
+
+    import torch
+    from raytracing_gpu_amd import assets
+
+    m = assets.door_mesh_from_fixture(os.path.join(os.path.dirname(__file__), "golden", "door_assimp.npz"))
+    img = assets.synthetic_image(2048, 2048) if scene == "door" else assets.synthetic_image(3410, 1518)
+    nfb = 2
+    gpu_ctx.upload(rtlib.Scene.builtin(scene, images=[img], meshes=[m]))
+    gpu_ctx.render_init(W, H, 1984)
+    fb = torch.zeros(nfb * H * W * 3, dtype=torch.float32, device="cuda")
+    gpu_ctx.render(rtlib.make_args(W, H, spp, 0, nfb, 50, REF), fb.data_ptr())
+    got = fb.cpu().numpy().reshape(nfb, H, W, 3)
+    ref = oracle.RefScene(scene, images=[img], meshes=[(m.tris, True, 0)])
+    js = list(range(rows[0], H, rows[1]))
+    for f in range(nfb):
+        want = ref.render(W, H, spp, f, 50, REF, rows=rows)[0].reshape(H, W, 3)
+        assert np.array_equal(_bits(got[f][js]), _bits(want[js])), f"{scene} fb {f}"
