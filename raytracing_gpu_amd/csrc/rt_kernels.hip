@@ -2100,6 +2100,7 @@ struct rt_ctx {
   uint32_t* jump_tab = nullptr;  // byte tables of the subsequence jumps (init_states_kernel)
   unsigned long long* work = nullptr;  // [0] work counter, [1..4] counters
   int32_t* row_map = nullptr;  // [rows] owned row -> image row, then [rows] processing order
+  std::vector<int32_t> row_map_host;  // what row_map holds (uploaded only when it changes)
   int row_cap = 0;
   unsigned long long* row_cost = nullptr;  // device, per image row
   int row_cost_cap = 0;
@@ -2830,6 +2831,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     if (c->row_map) HIPCHK(c, hipFree(c->row_map));
     c->row_map = nullptr;
     HIPCHK(c, hipMalloc((void**)&c->row_map, 2 * (size_t)rows * sizeof(int32_t)));
+    c->row_map_host.clear();
     c->row_cap = rows;
   }
   if (a->height > c->row_cost_cap) {
@@ -2871,9 +2873,15 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   if (const char* e = getenv("RT_COST_ORDER_ITEMS")) order_cap = atoll(e);  // tuning
   if (!sched && have_cost && items < order_cap)
     std::stable_sort(rm.begin() + rows, rm.end(), [&](int x, int y) { return c->host_cost[rm[x]] > c->host_cost[rm[y]]; });
-  HIPCHK(c, hipMemcpyAsync(c->row_map, rm.data(), 2 * (size_t)rows * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+  // Per-launch host work kept off the repeat path: the row tables are uploaded only when they
+  // change, the row costs are cleared and read back only on their measuring launch.
+  if (rm != c->row_map_host) {
+    c->row_map_host = rm;  // kept alive for the async copy
+    HIPCHK(c, hipMemcpyAsync(c->row_map, c->row_map_host.data(), 2 * (size_t)rows * sizeof(int32_t),
+                             hipMemcpyHostToDevice, c->stream));
+  }
   HIPCHK(c, hipMemsetAsync(c->work, 0, 8 * sizeof(unsigned long long), c->stream));
-  HIPCHK(c, hipMemsetAsync(c->row_cost, 0, (size_t)a->height * sizeof(unsigned long long), c->stream));
+  if (!have_cost) HIPCHK(c, hipMemsetAsync(c->row_cost, 0, (size_t)a->height * sizeof(unsigned long long), c->stream));
 
   RenderParams P{};
   P.S = c->scene;
@@ -3096,9 +3104,10 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
            (kVariants[var].mask & F_STEP) != 0 ? "render_step_kernel" : "render_kernel", kVariants[var].mask);
   unsigned long long host_cnt[8];
   HIPCHK(c, hipMemcpyAsync(host_cnt, c->work, sizeof(host_cnt), hipMemcpyDeviceToHost, c->stream));
-  std::vector<unsigned long long> cost((size_t)a->height);
-  HIPCHK(c, hipMemcpyAsync(cost.data(), c->row_cost, cost.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                           c->stream));
+  std::vector<unsigned long long> cost(have_cost ? 0 : (size_t)a->height);
+  if (!have_cost)
+    HIPCHK(c, hipMemcpyAsync(cost.data(), c->row_cost, cost.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                             c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (!have_cost) {
     c->host_cost.assign((size_t)a->height, 0ull);
