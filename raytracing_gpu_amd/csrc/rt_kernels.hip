@@ -715,24 +715,30 @@ __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r,
 // Camera-ray candidates of a world BVH from the per-tile candidate list (bin_tiles_kernel): every
 // primitive that any camera ray of the 8x8-pixel tile can hit, over the lens disk and the shutter,
 // is in the list, so the candidates of the culled search are all tested here instead of traversing
-// the tree; bvh_settle then decides the query exactly as after a traversal.
+// the tree; bvh_settle then decides the query exactly as after a traversal.  Entries are (primitive,
+// nearest) pairs sorted by `nearest`, a lower bound on the distance from the ray origin to any
+// point of the primitive: once nearest / |d| exceeds the winner's range end bhi (with the
+// traversal's 2^-8 margin) the remaining candidates lie beyond it -- a lo above bhi changes neither
+// the winner nor the certainty test second > bhi -- and the loop ends.  Two pairs per 16-byte load,
+// the next load issued before the current pair's tests; g0 = the first pair(s), loaded by the
+// caller together with the count.
 template <int F>
 __device__ __forceinline__ void tile_candidates(const DScene& S, const int32_t* __restrict__ ent, int cnt, int4 g0,
                                                 const Ray& r, float a, float rcpa, float tmin, float tmax,
                                                 float& blo, float& bhi, float& second, int& best_prim,
                                                 int& best_rank, unsigned& nprim) {
-  // Entries four at a time (one 16-byte global load per group instead of one load per entry), the
-  // next group's load issued before the current group's tests.  g0 = the first group, loaded by the
-  // caller together with the count.
+  const float rlen = __builtin_amdgcn_rsqf(a) * 0.99951171875f;  // 1/|d|, rounded well down (1 - 2^-11)
   const int4* __restrict__ e4 = reinterpret_cast<const int4*>(ent);
   int4 gn = g0;
-  for (int k = 0; k < cnt; k += 4) {
+  for (int k = 0; k < cnt; k += 2) {
     const int4 g = gn;
-    if (k + 4 < cnt) gn = e4[(k >> 2) + 1];
+    if (k + 2 < cnt) gn = e4[(k >> 1) + 1];
+    if (__int_as_float(g.y) * rlen > bhi * 1.00390625f) break;  // sorted: the rest lie beyond the winner
     #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 2; ++u) {
       if (k + u < cnt) {
-        const int pi = u == 0 ? g.x : (u == 1 ? g.y : (u == 2 ? g.z : g.w));
+        const int pi = u == 0 ? g.x : g.z;
+        if (u == 1 && __int_as_float(g.w) * rlen > bhi * 1.00390625f) break;
         const PrimRec q = load_prim<F>(S, pi);
         float lo, hi;
         if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim))
@@ -1304,7 +1310,8 @@ struct RenderParams {
   float* contrib;
   const uint4* cam_st;
   // Camera-ray candidate lists (render_step_kernel; null: camera rays traverse the tree): per 8x8
-  // tile of the image, tile_cnt[t] entries at tile_ent[t * tile_cap] (-1: the tile overflowed).
+  // tile of the image, tile_cnt[t] (id, nearest) pairs at tile_ent[2 * t * tile_cap] (-1: the tile
+  // overflowed).
   const int32_t* tile_cnt;
   const int32_t* tile_ent;
   int tiles_x, tile_cap;
@@ -1785,7 +1792,7 @@ void render_step_kernel(const RenderParams P) {
         int4 g0 = make_int4(0, 0, 0, 0);
         if (listed) {
           const int t = (j >> kTileShift) * P.tiles_x + (i >> kTileShift);
-          ent = P.tile_ent + (size_t)t * P.tile_cap;
+          ent = P.tile_ent + (size_t)t * P.tile_cap * 2;  // (id, nearest) pairs
           tcnt = P.tile_cnt[t];
           g0 = *reinterpret_cast<const int4*>(ent);
         }
@@ -2031,6 +2038,16 @@ struct TileFrustum {
     for (int c = 0; c < 4; ++c)
       for (int k = 0; k < 3; ++k) ok = ok && N[c][k] == N[c][k];
   }
+  // Lower bound on |p - o| for any point p of sphere s and any camera ray origin o = O + off
+  // (|off| <= L): |C - O| - R - L, rounded down (cast and a 1e-5 relative margin).  A camera ray's
+  // hit parameter t is then >= nearest / |d| (p = o + t d).
+  __device__ float nearest(float4 s) const {
+    const double C[3] = {s.x - O[0], s.y - O[1], s.z - O[2]};
+    const double dist = sqrt(C[0] * C[0] + C[1] * C[1] + C[2] * C[2]);
+    const double m = dist - s.w - L - 1e-5 * (dist + s.w + L) - 1e-6;
+    if (!(m == m)) return -__builtin_inff();
+    return __double2float_rd(m);
+  }
   // May a camera ray of the tile hit something inside sphere s (xyz centre, w radius)?
   __device__ bool sees(float4 s) const {
     const double C[3] = {s.x - O[0], s.y - O[1], s.z - O[2]};
@@ -2054,12 +2071,22 @@ __global__ __launch_bounds__(kBlock) void bin_tiles_kernel(const float4* __restr
   TileFrustum fr;
   fr.init(cam, W, H, t, tx);
   int c = 0;
+  int32_t* e = ent + (size_t)t * kTileCap * 2;  // (primitive id, nearest distance bits) pairs
   if (!fr.ok) {
     c = kTileCap + 1;
   } else {
     for (int q = 0; q < n; ++q)
       if (fr.sees(sph[q])) {
-        if (c < kTileCap) ent[(size_t)t * kTileCap + c] = ids[q];
+        if (c < kTileCap) {  // insertion by the nearest possible hit distance, ascending
+          const float dn = fr.nearest(sph[q]);
+          int k = c;
+          for (; k > 0 && __int_as_float(e[2 * k - 1]) > dn; --k) {
+            e[2 * k] = e[2 * k - 2];
+            e[2 * k + 1] = e[2 * k - 1];
+          }
+          e[2 * k] = ids[q];
+          e[2 * k + 1] = __float_as_int(dn);
+        }
         ++c;
       }
   }
@@ -3039,12 +3066,12 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   if (cull && (vm & F_STEP) != 0 && c->bin_n > 0 && (double)P.total_items >= bins_min * lanes) {
     const long long tkey[3] = {c->scene_gen, a->width, a->height};
     if (!std::equal(tkey, tkey + 3, c->tiles_key)) {
-      if (ntp + nt * kTileCap > c->tiles_cap) {
+      if (ntp + nt * kTileCap * 2 > c->tiles_cap) {
         if (c->tiles) HIPCHK(c, hipFree(c->tiles));
         c->tiles = nullptr;
         c->tiles_cap = 0;
-        HIPCHK(c, hipMalloc((void**)&c->tiles, (size_t)(ntp + nt * kTileCap) * sizeof(int32_t)));
-        c->tiles_cap = ntp + nt * kTileCap;
+        HIPCHK(c, hipMalloc((void**)&c->tiles, (size_t)(ntp + nt * kTileCap * 2) * sizeof(int32_t)));
+        c->tiles_cap = ntp + nt * kTileCap * 2;
       }
       bin_tiles_kernel<<<(unsigned)((nt + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
           c->bin_sph, c->bin_ids, c->bin_n, c->scene.cam, a->width, a->height, tx, ty, c->tiles, c->tiles + ntp);
