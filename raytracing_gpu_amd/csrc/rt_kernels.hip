@@ -755,7 +755,8 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
                                            bool overflow, float bhi, float second, float& best, int& best_prim,
                                            int best_rank, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   const int last0 = (1 << (rows - 1)) - 1;
-  const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+  // the reference's reciprocals (three IEEE divides), only on the rare paths that test boxes
+  auto inv_of = [&r]() { return mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z); };
   // The candidate search keeps ranges: its winner is certain when every other candidate's range
   // lies above the winner's (second > bhi), and its exact t (the reference's hit() value) must
   // pass [tmin, tmax].  Otherwise -- a subtree dropped on stack overflow, overlapping ranges (near
@@ -770,12 +771,12 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
   }
   if (!sure) {
     if constexpr ((F & F_STATS) != 0) ++nfall;
-    return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
+    return bvh_exact<F>(S, base, rows, r, inv_of(), tmin, tmax, best, best_prim, nnode, nprim, nfall);
   }
   if constexpr ((F & F_CHECK) != 0) {
     float te;
     int pe;
-    bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, te, pe, nnode, nprim, nfall);
+    bvh_exact<F>(S, base, rows, r, inv_of(), tmin, tmax, te, pe, nnode, nprim, nfall);
     if (pe != best_prim || (pe >= 0 && __float_as_uint(te) != __float_as_uint(best))) {
       const unsigned slot = atomicAdd(S.dbg_n, 1u);
       if ((int)slot < S.dbg_cap) {
@@ -819,6 +820,7 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
   }
   const float2 pm = pmargin_of<F>(S)[best_prim];
   const unsigned must = bound < pm.y ? __float_as_uint(pm.x) : 0xffffffffu;
+  const V inv = inv_of();
   int pos = 0;
   for (int kr = last0 + (best_rank >> 1);; kr = (kr - 1) >> 1, ++pos) {
     if ((must >> pos) & 1u) {
@@ -1825,7 +1827,9 @@ void render_step_kernel(const RenderParams P) {
           ray.tm = urange(cr, C.time0, C.time1);
           att = mk(1.0f, 1.0f, 1.0f);
         }
-        const V inv = mk(1.0f / ray.d.x, 1.0f / ray.d.y, 1.0f / ray.d.z);
+        // traversal reciprocals: hardware v_rcp_f32 (1 ulp; the tree's boxes are padded by 2^-16
+        // relative, far above either reciprocal's rounding) instead of three IEEE divides
+        const V inv = mk(__builtin_amdgcn_rcpf(ray.d.x), __builtin_amdgcn_rcpf(ray.d.y), __builtin_amdgcn_rcpf(ray.d.z));
         finv = mk(__builtin_fminf(__builtin_fmaxf(inv.x, -1e30f), 1e30f),
                   __builtin_fminf(__builtin_fmaxf(inv.y, -1e30f), 1e30f),
                   __builtin_fminf(__builtin_fmaxf(inv.z, -1e30f), 1e30f));
