@@ -849,11 +849,13 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
 template <int F>
 __device__ __forceinline__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, float tmin, float tmax, float& best,
                             int& best_prim, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
-  const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
   const int base = o.a, rows = o.b;
   if constexpr ((F & F_EXACT) != 0) {
+    const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);  // the reference's reciprocals
     return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
   } else {
+    // traversal reciprocals from v_rcp_f32 (see render_step_kernel's query setup)
+    const V inv = mk(__builtin_amdgcn_rcpf(r.d.x), __builtin_amdgcn_rcpf(r.d.y), __builtin_amdgcn_rcpf(r.d.z));
     const int fb = o.c;  // traversal tree: 64-byte records at nodes[fb + 2i], root i = 0
     // Finite reciprocals for the traversal tree: with d = 0 the fma form would give inf - inf.
     // Clamped to +-1e30 the slab of a parallel axis is (-huge, +huge) inside and empty outside.
