@@ -2813,7 +2813,8 @@ int rt_render_init(rt_ctx* c, int32_t width, int32_t height, uint64_t seed) {
   hipLaunchKernelGGL(init_states_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, c->states, n, seed,
                      (const uint32_t*)c->jump_tab, digits);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  // no host wait: every reader of the states (rt_render's kernels, rt_read_states) is ordered
+  // after this launch on the context's stream
   c->states_seed = seed;
   return RT_OK;
 }
@@ -3191,7 +3192,9 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     // 12); at N = 1 and 2 a fixed 24 costs 3.5 % and 2 % (the split samples' extra claims and
     // state loads), hence the rule by share size.
     {
-      const double lanes = (double)c->cus * std::max(1, c->blocks_per_cu[var]) * bs;
+      // lanes of the stepwise kernel that runs the split launches (4 waves/SIMD: 1024 per CU),
+      // whatever variant measured (bench.py measures with the counting variant)
+      const double lanes = (double)c->cus * 1024.0;
       double thr = (double)items < 6.0 * lanes ? 24.0 : std::max(32.0, 0.5 * (double)host_cnt[1] / lanes);
       if (const char* e = getenv("RT_SPLIT_MIN_SEGMENTS")) thr = atof(e);  // tuning
       const long long bt = (long long)std::ceil(thr / (double)(1 << shift));
@@ -3266,7 +3269,9 @@ int rt_read_states(rt_ctx* c, int64_t first, int64_t count, uint32_t* out) {
   if (!c->states || first + count > c->states_n) return fail(c, RT_ERR_STATE, "states not initialised");
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<uint4> tmp((size_t)count * 2);
-  HIPCHK(c, hipMemcpy(tmp.data(), c->states + 2 * first, tmp.size() * sizeof(uint4), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpyAsync(tmp.data(), c->states + 2 * first, tmp.size() * sizeof(uint4), hipMemcpyDeviceToHost,
+                           c->stream));  // after rt_render_init's kernel on the same stream
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   for (int64_t k = 0; k < count; ++k) {
     const uint4 a = tmp[2 * k], b = tmp[2 * k + 1];
     const uint32_t w[6] = {a.x, a.y, a.z, a.w, b.x, b.y};
