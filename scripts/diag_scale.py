@@ -32,7 +32,17 @@ def timed(fn):
     return ev[0].elapsed_time(ev[1])
 
 
-t_init = min(timed(lambda: ctx.render_init(W, H, 1984)) for _ in range(3))
+def host_timed(fn):  # render_init runs on the context's own stream: time it to a device-wide sync
+    import time
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3
+
+
+t_init = min(host_timed(lambda: ctx.render_init(W, H, 1984)) for _ in range(5))
 xgmi = float(os.environ.get("XGMI_GBS", "64"))
 base = None
 for n in (1, 2, 4, 8):
