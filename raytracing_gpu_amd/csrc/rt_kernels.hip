@@ -2147,6 +2147,8 @@ struct rt_ctx {
   uint32_t* perm = nullptr;
   long long item_cap = 0;
   long long perm_key[10] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+  long long pending_key[10] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1};  // measured, schedule not built yet
+  unsigned long long pending_segs = 0;
   unsigned long long n_long = 0;
   // Split samples of the longest items (render_step_kernel; see rt_render): n_split perm positions,
   // split_state 0 = record on the next launch of perm_key, 1 = recorded for split_seed.
@@ -2484,6 +2486,67 @@ void camera_table(const rt_camera& C, uint64_t seed, int spp, std::vector<float4
     const float tm = C.time0 + (C.time1 - C.time0) * rtx::uniform(cr);
     out[(size_t)s] = make_float4(ox, oy, oz, tm);
   }
+}
+
+// Item schedule of a configuration from its measuring launch's per-item segment counts (c->item_cost,
+// `segs` segments in all): perm, the long prefix and the split items.  Built when the configuration
+// is rendered again, so a single draw() does not pay the host sort.
+int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs) {
+  std::vector<uint16_t> ic((size_t)items);
+  HIPCHK(c, hipMemcpyAsync(ic.data(), c->item_cost, ic.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (const char* e = getenv("RT_ITEM_COST_OUT")) {  // diagnostic: per-item segment counts
+    if (FILE* fo = fopen(e, "wb")) {
+      fwrite(ic.data(), sizeof(uint16_t), ic.size(), fo);
+      fclose(fo);
+    }
+  }
+  // Every item in descending cost buckets of 8 segments, the natural (spatially coherent) order
+  // inside a bucket; the top ~2 % by cost are the "long" prefix whose waves run at raised
+  // priority.  (C2, one GPU as rank 0 of N: N = 8 share 3.89 -> 3.45 ms, N = 1 unchanged.)
+  int shift = 3;
+  if (const char* e = getenv("RT_COST_SHIFT")) shift = std::max(0, std::min(12, atoi(e)));  // tuning
+  for (uint16_t& v : ic) v = (uint16_t)(v >> shift);
+  std::vector<long long> hist(65536, 0);
+  for (uint16_t v : ic) ++hist[v];
+  std::vector<long long> start(65536, 0);  // counting sort, highest bucket first
+  long long acc = 0;
+  for (int v = 65535; v >= 0; --v) {
+    start[v] = acc;
+    acc += hist[v];
+  }
+  double pct = 2.0;
+  if (const char* e = getenv("RT_LONG_PCT")) pct = atof(e);  // tuning
+  const long long want = (long long)((double)items * pct / 100.0);
+  long long nl = 0;  // whole buckets from the top while they fit in `want`
+  for (int v = 65535; v >= 0 && nl + hist[v] <= want; --v) nl += hist[v];
+  std::vector<uint32_t> pm((size_t)items);
+  for (long long k = 0; k < items; ++k) pm[(size_t)start[ic[(size_t)k]]++] = (uint32_t)k;
+  // on the context's stream, completed before returning: the next launch (same stream) reads it
+  HIPCHK(c, hipMemcpyAsync(c->perm, pm.data(), pm.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->n_long = (unsigned long long)nl;
+  // Items that can decide when a launch ends have their samples split on later launches: in a
+  // small share (< 6 items per resident lane, as for the camera lists) every item of >= 24
+  // segments, else items longer than half a resident lane's share of the segments (at least 32).
+  // They are the first positions of perm (cost buckets descending).  C2, one GPU per rank's
+  // share: N = 8 share 3.59 -> 2.88 ms with 24 (3.34 ms with the large-share rule, 3.15 with
+  // 12); at N = 1 and 2 a fixed 24 costs 3.5 % and 2 % (the split samples' extra claims and
+  // state loads), hence the rule by share size.
+  {
+    // lanes of the stepwise kernel that runs the split launches (4 waves/SIMD: 1024 per CU),
+    // whatever variant measured (bench.py measures with the counting variant)
+    const double lanes = (double)c->cus * 1024.0;
+    double thr = (double)items < 6.0 * lanes ? 24.0 : std::max(32.0, 0.5 * (double)segs / lanes);
+    if (const char* e = getenv("RT_SPLIT_MIN_SEGMENTS")) thr = atof(e);  // tuning
+    const long long bt = (long long)std::ceil(thr / (double)(1 << shift));
+    long long ns = 0;
+    for (long long v = 65535; v >= bt && v >= 0; --v) ns += hist[(size_t)v];
+    if (ns * (long long)spp >= (1LL << 30)) ns = 0;
+    c->n_split = (unsigned long long)ns;
+    c->split_state = ns > 0 ? 0 : -1;
+  }
+  return RT_OK;
 }
 
 int validate_args(rt_ctx* c, const rt_render_args* a) {
@@ -2891,6 +2954,12 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   const long long pkey[10] = {c->scene_gen, a->width, a->height, a->spp, a->max_depth,
                               a->fb_first, a->fb_count, a->band_rows, a->band_first, a->band_stride};
   const bool sched = items <= (64LL << 20) && (a->flags & RT_FLAG_NO_SCHEDULE) == 0;
+  if (sched && !std::equal(pkey, pkey + 10, c->perm_key) && std::equal(pkey, pkey + 10, c->pending_key) &&
+      items <= c->item_cap) {  // the configuration repeats: its schedule from the measured counts
+    if ((rc = build_schedule(c, items, a->spp, c->pending_segs))) return rc;
+    std::copy(pkey, pkey + 10, c->perm_key);
+    std::fill(c->pending_key, c->pending_key + 10, -1LL);
+  }
   const bool have_perm = sched && std::equal(pkey, pkey + 10, c->perm_key);
   if (sched && items > c->item_cap) {
     if (c->item_cost) HIPCHK(c, hipFree(c->item_cost));
@@ -2899,6 +2968,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     c->perm = nullptr;
     c->item_cap = 0;
     std::fill(c->perm_key, c->perm_key + 10, -1LL);
+    std::fill(c->pending_key, c->pending_key + 10, -1LL);
     HIPCHK(c, hipMalloc((void**)&c->item_cost, (size_t)items * sizeof(uint16_t)));
     HIPCHK(c, hipMalloc((void**)&c->perm, (size_t)items * sizeof(uint32_t)));
     c->item_cap = items;
@@ -3149,62 +3219,9 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   }
   if (!have_cost)
     for (int q = 0; q < rows; ++q) c->host_cost[rm[q]] = cost[rm[q]];
-  if (sched && !have_perm) {  // build the schedule of the next launches of this configuration
-    std::vector<uint16_t> ic((size_t)items);
-    HIPCHK(c, hipMemcpyAsync(ic.data(), c->item_cost, ic.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (const char* e = getenv("RT_ITEM_COST_OUT")) {  // diagnostic: per-item segment counts
-      if (FILE* fo = fopen(e, "wb")) {
-        fwrite(ic.data(), sizeof(uint16_t), ic.size(), fo);
-        fclose(fo);
-      }
-    }
-    // Every item in descending cost buckets of 8 segments, the natural (spatially coherent) order
-    // inside a bucket; the top ~2 % by cost are the "long" prefix whose waves run at raised
-    // priority.  (C2, one GPU as rank 0 of N: N = 8 share 3.89 -> 3.45 ms, N = 1 unchanged.)
-    int shift = 3;
-    if (const char* e = getenv("RT_COST_SHIFT")) shift = std::max(0, std::min(12, atoi(e)));  // tuning
-    for (uint16_t& v : ic) v = (uint16_t)(v >> shift);
-    std::vector<long long> hist(65536, 0);
-    for (uint16_t v : ic) ++hist[v];
-    std::vector<long long> start(65536, 0);  // counting sort, highest bucket first
-    long long acc = 0;
-    for (int v = 65535; v >= 0; --v) {
-      start[v] = acc;
-      acc += hist[v];
-    }
-    double pct = 2.0;
-    if (const char* e = getenv("RT_LONG_PCT")) pct = atof(e);  // tuning
-    const long long want = (long long)((double)items * pct / 100.0);
-    long long nl = 0;  // whole buckets from the top while they fit in `want`
-    for (int v = 65535; v >= 0 && nl + hist[v] <= want; --v) nl += hist[v];
-    std::vector<uint32_t> pm((size_t)items);
-    for (long long k = 0; k < items; ++k) pm[(size_t)start[ic[(size_t)k]]++] = (uint32_t)k;
-    // on the context's stream, completed before returning: the next launch (same stream) reads it
-    HIPCHK(c, hipMemcpyAsync(c->perm, pm.data(), pm.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->n_long = (unsigned long long)nl;
-    // Items that can decide when a launch ends have their samples split on later launches: in a
-    // small share (< 6 items per resident lane, as for the camera lists) every item of >= 24
-    // segments, else items longer than half a resident lane's share of the segments (at least 32).
-    // They are the first positions of perm (cost buckets descending).  C2, one GPU per rank's
-    // share: N = 8 share 3.59 -> 2.88 ms with 24 (3.34 ms with the large-share rule, 3.15 with
-    // 12); at N = 1 and 2 a fixed 24 costs 3.5 % and 2 % (the split samples' extra claims and
-    // state loads), hence the rule by share size.
-    {
-      // lanes of the stepwise kernel that runs the split launches (4 waves/SIMD: 1024 per CU),
-      // whatever variant measured (bench.py measures with the counting variant)
-      const double lanes = (double)c->cus * 1024.0;
-      double thr = (double)items < 6.0 * lanes ? 24.0 : std::max(32.0, 0.5 * (double)host_cnt[1] / lanes);
-      if (const char* e = getenv("RT_SPLIT_MIN_SEGMENTS")) thr = atof(e);  // tuning
-      const long long bt = (long long)std::ceil(thr / (double)(1 << shift));
-      long long ns = 0;
-      for (long long v = 65535; v >= bt && v >= 0; --v) ns += hist[(size_t)v];
-      if (ns * (long long)a->spp >= (1LL << 30)) ns = 0;
-      c->n_split = (unsigned long long)ns;
-      c->split_state = ns > 0 ? 0 : -1;
-    }
-    std::copy(pkey, pkey + 10, c->perm_key);
+  if (sched && !have_perm) {  // the schedule is built from these counts when the configuration repeats
+    std::copy(pkey, pkey + 10, c->pending_key);
+    c->pending_segs = host_cnt[1];
   }
   if (split_mode == 1) {  // sample-start states recorded for this seed
     c->split_state = 1;
