@@ -2985,7 +2985,9 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
                              hipMemcpyHostToDevice, c->stream));
   }
   HIPCHK(c, hipMemsetAsync(c->work, 0, 8 * sizeof(unsigned long long), c->stream));
-  if (!have_cost) HIPCHK(c, hipMemsetAsync(c->row_cost, 0, (size_t)a->height * sizeof(unsigned long long), c->stream));
+  // row costs order the rows only when there is no item schedule: measured only then
+  const bool measure_rows = !have_cost && !sched;
+  if (measure_rows) HIPCHK(c, hipMemsetAsync(c->row_cost, 0, (size_t)a->height * sizeof(unsigned long long), c->stream));
 
   RenderParams P{};
   P.S = c->scene;
@@ -2993,7 +2995,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   P.fb = fb_dev;
   P.row_map = c->row_map;
   P.row_order = c->row_map + rows;
-  P.row_cost = have_cost ? nullptr : c->row_cost;  // measured once per configuration
+  P.row_cost = measure_rows ? c->row_cost : nullptr;  // measured once per configuration
   P.work = c->work;
   P.counters = c->work + 1;
   P.total_items = (unsigned long long)a->fb_count * rows * a->width;
@@ -3208,17 +3210,16 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
            (kVariants[var].mask & F_STEP) != 0 ? "render_step_kernel" : "render_kernel", kVariants[var].mask);
   unsigned long long host_cnt[8];
   HIPCHK(c, hipMemcpyAsync(host_cnt, c->work, sizeof(host_cnt), hipMemcpyDeviceToHost, c->stream));
-  std::vector<unsigned long long> cost(have_cost ? 0 : (size_t)a->height);
-  if (!have_cost)
+  std::vector<unsigned long long> cost(measure_rows ? (size_t)a->height : 0);
+  if (measure_rows)
     HIPCHK(c, hipMemcpyAsync(cost.data(), c->row_cost, cost.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                              c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (!have_cost) {
+  if (measure_rows) {
     c->host_cost.assign((size_t)a->height, 0ull);
     std::copy(key, key + 5, c->cost_key);
-  }
-  if (!have_cost)
     for (int q = 0; q < rows; ++q) c->host_cost[rm[q]] = cost[rm[q]];
+  }
   if (sched && !have_perm) {  // the schedule is built from these counts when the configuration repeats
     std::copy(pkey, pkey + 10, c->pending_key);
     c->pending_segs = host_cnt[1];
