@@ -93,10 +93,14 @@ def parse():
     ap.add_argument("--no-lds", action="store_true", help="keep the scene in global memory")
     ap.add_argument("--no-step", action="store_true", help="segment-per-trip kernel even when the world is one BVH")
     ap.add_argument("--no-bins", action="store_true", help="camera rays traverse the BVH (no per-tile candidate lists)")
+    ap.add_argument("--no-schedule", action="store_true", help="every draw cold: nothing reused from an earlier launch")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the untimed node/prim counting pass")
     ap.add_argument("--png", default="", help="write the assembled image (rank 0)")
+    ap.add_argument("--cold-steps", type=int, default=3, help="draws timed with nothing reused (cold_ms_per_step)")
+    ap.add_argument("--gather", default="rccl", choices=["rccl", "host"],
+                    help="--gpus N without a launcher: ncclGather over distinct devices, or host copies (ranks may share a GPU)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="debug: gloo runs the N>1 path with host-side collectives and ranks sharing the visible GPUs")
     return ap.parse_args()
@@ -158,18 +162,99 @@ def cpu_baseline(a, budget_s: float) -> dict:
                       f"{segs} segments in {dt:.1f} s, {threads} threads (oracle/ref_cpu.cpp, g++ -O2)"}
 
 
+def roofline(a, stats, kname, avg_ms, rows, workload, world):
+    """roofline object of the dominant kernel (render) from this run's live kernel time, the
+    untimed stats pass's node/prim counts and, when committed for this exact build, its PMC summary."""
+    if stats is None:
+        return None
+    items = a.nfb * rows * a.width
+    bytes_launch = NODE_BYTES * stats["node_tests"] + PRIM_BYTES * stats["prim_tests"] + ITEM_BYTES * items
+    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+    # LDS / memory roof of the algorithmic bytes (SURVEY.md 8d: node + primitive records + per-item
+    # state and fb bytes).  The LDS variants read node/primitive records from the workgroup's
+    # LDS copy of the scene, the others from L2 / HBM.
+    mem = {"achieved": round(achieved, 2), "unit": "GB/s", "bytes_per_launch": int(bytes_launch),
+           "bytes_per_segment": round(bytes_launch / max(stats["segments"], 1), 2),
+           "node_tests_per_segment": round(stats["node_tests"] / max(stats["segments"], 1), 3),
+           "prim_tests_per_segment": round(stats["prim_tests"] / max(stats["segments"], 1), 3)}
+    if lds_variant(kname):
+        mem.update(served_from="LDS", peak=round(LDS_PEAK_GBS, 1), frac=round(achieved / LDS_PEAK_GBS, 4))
+        roof = {"bound": "lds", "achieved": mem["achieved"], "peak": mem["peak"], "unit": "GB/s", "frac": mem["frac"]}
+    else:
+        # node/primitive records come from L2 (the scenes are a few MB): against the HBM peak the
+        # ratio can exceed 1, so it is not reported as a roofline fraction; the binding roof needs
+        # this build's PMC summary (below)
+        mem.update(served_from="L2 (scene), HBM (RNG states, fb)", hbm_peak=HBM_PEAK_GBS,
+                   ratio_to_hbm_peak=round(achieved / HBM_PEAK_GBS, 4))
+        roof = {"bound": "unmeasured (no PMC summary for this build)", "achieved": None, "peak": None,
+                "unit": None, "frac": None}
+    roof.update({"traffic": None, "kernel": kname, "kernel_avg_ms": round(avg_ms, 3),
+                 "fallbacks": stats["fallbacks"], "algorithmic": mem})
+    pmc, bid = committed_pmc(workload, kname) if world == 1 else (None, None)
+    roof["build_id"] = bid
+    if pmc is not None:
+        src, d = pmc
+        # Counters are per launch of this same build and workload (rocprofv3 --pmc passes,
+        # scripts/profile.sh); rates use this run's live kernel time.
+        hbm = d["hbm_bytes_per_launch"]  # 2*FETCH_SIZE + WRITE_SIZE (gfx950 correction)
+        roof["traffic"] = hbm
+        roof["hbm"] = {"achieved": round(hbm / (avg_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(hbm / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+        roof["pmc_source"] = src
+        roof["pmc_git_head"] = d.get("git_head")
+        roof["pmc_note"] = "counters committed for this build_id, measured in a separate rocprofv3 run, not this one"
+        if "SQ_INSTS_VALU" in d:
+            # binding roof of the megakernel: VALU issue (no MFMA: no dense contraction; the scene
+            # is LDS/L2-resident, so HBM and the LDS array are far from their roofs)
+            rate = d["SQ_INSTS_VALU"] / (avg_ms * 1e-3) / 1e9
+            peak = VALU_ISSUE_PER_S / 1e9
+            roof.update(bound="valu", achieved=round(rate, 2), peak=round(peak, 1),
+                        unit="G wave64-VALU-inst/s", frac=round(rate / peak, 4))
+            roof["valu"] = {"insts_per_launch": int(d["SQ_INSTS_VALU"]),
+                            "lane_utilisation": round(d.get("valu_lane_utilisation", float("nan")), 4)}
+            if "SQ_WAIT_ANY" in d and "SQ_WAVE_CYCLES" in d:
+                roof["valu"]["wait_any_share"] = round(d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"], 4)
+            if "SQ_LDS_BANK_CONFLICT" in d and "SQ_LDS_IDX_ACTIVE" in d:
+                roof["valu"]["lds_bank_conflict_share"] = round(
+                    d["SQ_LDS_BANK_CONFLICT"] / max(d["SQ_LDS_IDX_ACTIVE"], 1), 4)
+    return roof
+
+
+def workload_name(a) -> str:
+    return (f"{CONFIG_OF.get(a.scene, 'scene')} {a.scene} {a.width}x{a.height}, {a.nfb} fb x {a.spp} spp = "
+            f"{a.nfb * a.spp} rays/pixel, depth {a.depth}, cam {a.cam}, traversal {'exact' if a.exact else 'culled'}"
+            f"{'' if not a.no_lds else ', global scene'}")
+
+
+def out_line(a, value, world, dt_step, segs, roof, extra):
+    out = {
+        "metric": "Mrays/sec (primary+bounces) on RTIOW random-spheres 1200x800x100spp",
+        "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(dt_step * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic (reference scene generator, seed 1984)",
+        "config": {"workload": workload_name(a),
+                   "scene": a.scene, "width": a.width, "height": a.height, "rays_per_pixel": a.nfb * a.spp,
+                   "no_fb": a.nfb, "spp_per_fb": a.spp, "max_depth": a.depth,
+                   "segments_per_step": int(segs), "parallelism": f"rows{world}"},
+        "roofline": roof,
+    }
+    out.update(extra)
+    return out
+
+
 def main():
     a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return main_inprocess(a)  # the C++ multi-GPU driver, one process, one thread per rank
+    if a.gpus != world:
+        raise SystemExit(f"bench.py --gpus {a.gpus} but WORLD_SIZE={world}")
     import torch
     import torch.distributed as dist
 
     import raytracing_gpu_amd as rt
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if a.gpus != world:
-        raise SystemExit(f"bench.py --gpus {a.gpus} but WORLD_SIZE={world}: launch N > 1 with "
-                         f"torch.distributed.run --nproc-per-node {a.gpus}")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.backend == "gloo":  # rehearsal on fewer GPUs than ranks: ranks share devices
         local = local % max(1, torch.cuda.device_count())
@@ -183,9 +268,10 @@ def main():
     sc = rt.Scene.builtin(a.scene, **scene_assets(a.scene)[0])
     ctx.upload(sc)
     cam = rt.RT_CAM_REF_SLOT0 if a.cam == "ref" else rt.RT_CAM_PER_PIXEL
-    args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, band_rows=a.band_rows,
-                        band_first=rank, band_stride=world, exact=a.exact, lds=not a.no_lds,
-                        step=not a.no_step, bins=not a.no_bins)
+    kw = dict(band_rows=a.band_rows, band_first=rank, band_stride=world, exact=a.exact, lds=not a.no_lds,
+              step=not a.no_step, bins=not a.no_bins)
+    args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, schedule=not a.no_schedule, **kw)
+    cold_args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, schedule=False, **kw)
     rows = rt.owned_rows(args)
     all_rows = []
     for r in range(world):
@@ -197,6 +283,49 @@ def main():
     img = torch.zeros(max_rows * a.width * 3, dtype=torch.uint8, device=dev)
     gathered = torch.empty(world * img.numel(), dtype=torch.uint8, device=cdev) if world > 1 else None
 
+    seg_step = [0]
+    kms = []
+    kname = [""]
+    sched = []
+
+    def step(args_):
+        ctx.render_init(a.width, a.height, 1984)
+        cnt = ctx.render(args_, fb.data_ptr())
+        kms.append(ctx.last_render_ms())
+        kname[0] = ctx.last_render_kernel()
+        sched.append(ctx.last_render_schedule())
+        ctx.resolve(args_, fb.data_ptr(), img.data_ptr())
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, img.to(cdev))
+        seg_step[0] = cnt["segments"]
+        return cnt
+
+    def timed(n, args_):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            step(args_)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0
+
+    # module load + first allocations, on a tiny image (a different configuration: the schedule
+    # of the measured one stays cold)
+    ctx.render_init(64, 36, 1984)
+    tiny = rt.make_args(64, 36, 1, 0, 1, a.depth, cam)
+    tfb = torch.empty(64 * 36 * 3, dtype=torch.float32, device=dev)
+    ctx.render(tiny, tfb.data_ptr())
+    # cold draws: nothing reused from an earlier launch (RT_FLAG_NO_SCHEDULE), as one draw() runs
+    step(cold_args)
+    kms.clear()
+    sched.clear()
+    dt_cold = timed(max(1, a.cold_steps), cold_args) / max(1, a.cold_steps)
+    cold_kms = sum(kms) / len(kms)
+    assert all(x == 0 for x in sched), sched
+
     stats = None
     if not a.no_stats:  # untimed pass of the counting variant: node / prim tests for B_seg
         ctx.render_init(a.width, a.height, 1984)
@@ -204,113 +333,33 @@ def main():
                              band_first=rank, band_stride=world, stats=True, exact=a.exact)
         stats = ctx.render(sargs, fb.data_ptr())
 
-    seg_step = [0]
-    kms = []
-    kname = [""]
-
-    def step():
-        ctx.render_init(a.width, a.height, 1984)
-        cnt = ctx.render(args, fb.data_ptr())
-        kms.append(ctx.last_render_ms())
-        kname[0] = ctx.last_render_kernel()
-        ctx.resolve(args, fb.data_ptr(), img.data_ptr())
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, img.to(cdev))
-        seg_step[0] = cnt["segments"]
-        return cnt
-
     for _ in range(a.warmup):
-        step()
+        step(args)
     kms.clear()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    sched.clear()
+    dt = timed(a.steps, args)
 
     tot = torch.tensor([float(seg_step[0])], dtype=torch.float64, device=cdev)
-    tmax = torch.tensor([dt], dtype=torch.float64, device=cdev)
+    tmax = torch.tensor([dt, dt_cold], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     segs = float(tot.item())
-    dt = float(tmax.item())
+    dt, dt_cold = float(tmax[0].item()), float(tmax[1].item())
     value = segs * a.steps / dt / 1e6
 
     if rank == 0:
         avg_ms = sum(kms) / len(kms)
-        roof = None
-        workload = (f"{CONFIG_OF.get(a.scene, 'scene')} {a.scene} {a.width}x{a.height}, {a.nfb} fb x {a.spp} spp = {a.nfb * a.spp} rays/pixel, "
-                    f"depth {a.depth}, cam {a.cam}, traversal {'exact' if a.exact else 'culled'}"
-                    f"{'' if not a.no_lds else ', global scene'}")
-        if stats is not None:
-            items = a.nfb * len(rows) * a.width
-            bytes_launch = NODE_BYTES * stats["node_tests"] + PRIM_BYTES * stats["prim_tests"] + ITEM_BYTES * items
-            achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
-            # LDS / memory roof of the algorithmic bytes (node + primitive records + per-item
-            # state and fb bytes).  The LDS variants read node/primitive records from the workgroup's
-            # LDS copy of the scene, the others from L2 / HBM.
-            mem = {"achieved": round(achieved, 2), "unit": "GB/s", "bytes_per_launch": int(bytes_launch),
-                   "bytes_per_segment": round(bytes_launch / max(stats["segments"], 1), 2),
-                   "node_tests_per_segment": round(stats["node_tests"] / max(stats["segments"], 1), 3),
-                   "prim_tests_per_segment": round(stats["prim_tests"] / max(stats["segments"], 1), 3)}
-            if lds_variant(kname[0]):
-                mem.update(served_from="LDS", peak=round(LDS_PEAK_GBS, 1), frac=round(achieved / LDS_PEAK_GBS, 4))
-                roof = {"bound": "lds", "achieved": mem["achieved"], "peak": mem["peak"], "unit": "GB/s",
-                        "frac": mem["frac"]}
-            else:
-                # node/primitive records come from L2 (the scenes are a few MB): against the HBM
-                # peak the ratio can exceed 1, so it is not reported as a roofline fraction; the
-                # binding roof needs this build's PMC summary (below)
-                mem.update(served_from="L2 (scene), HBM (RNG states, fb)", hbm_peak=HBM_PEAK_GBS,
-                           ratio_to_hbm_peak=round(achieved / HBM_PEAK_GBS, 4))
-                roof = {"bound": "unmeasured (no PMC summary for this build)", "achieved": None, "peak": None,
-                        "unit": None, "frac": None}
-            roof.update({"traffic": None, "kernel": kname[0], "kernel_avg_ms": round(avg_ms, 3),
-                         "fallbacks": stats["fallbacks"], "algorithmic": mem})
-            pmc, bid = committed_pmc(workload, kname[0]) if world == 1 else (None, None)
-            roof["build_id"] = bid
-            if pmc is not None:
-                src, d = pmc
-                # Counters are per launch of this same build and workload (rocprofv3 --pmc passes,
-                # scripts/profile.sh); rates use this run's live kernel time.
-                hbm = d["hbm_bytes_per_launch"]  # 2*FETCH_SIZE + WRITE_SIZE (gfx950 correction)
-                roof["traffic"] = hbm
-                roof["hbm"] = {"achieved": round(hbm / (avg_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": round(hbm / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
-                roof["pmc_source"] = src
-                roof["pmc_git_head"] = d.get("git_head")
-                roof["pmc_note"] = "counters committed for this build_id, measured in a separate rocprofv3 run, not this one"
-                if "SQ_INSTS_VALU" in d:
-                    # binding roof of the megakernel: VALU issue (no MFMA: no dense contraction; the
-                    # scene is LDS/L2-resident, so HBM and the LDS array are far from their roofs)
-                    rate = d["SQ_INSTS_VALU"] / (avg_ms * 1e-3) / 1e9
-                    peak = VALU_ISSUE_PER_S / 1e9
-                    roof.update(bound="valu", achieved=round(rate, 2), peak=round(peak, 1),
-                                unit="G wave64-VALU-inst/s", frac=round(rate / peak, 4))
-                    roof["valu"] = {"insts_per_launch": int(d["SQ_INSTS_VALU"]),
-                                    "lane_utilisation": round(d.get("valu_lane_utilisation", float("nan")), 4)}
-                    if "SQ_WAIT_ANY" in d and "SQ_WAVE_CYCLES" in d:
-                        roof["valu"]["wait_any_share"] = round(d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"], 4)
-                    if "SQ_LDS_BANK_CONFLICT" in d and "SQ_LDS_IDX_ACTIVE" in d:
-                        roof["valu"]["lds_bank_conflict_share"] = round(
-                            d["SQ_LDS_BANK_CONFLICT"] / max(d["SQ_LDS_IDX_ACTIVE"], 1), 4)
-        out = {
-            "metric": "Mrays/sec (primary+bounces) on RTIOW random-spheres 1200x800x100spp",
-            "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic (reference scene generator, seed 1984)",
-            "config": {"workload": workload,
-                       "scene": a.scene, "width": a.width, "height": a.height, "rays_per_pixel": a.nfb * a.spp,
-                       "no_fb": a.nfb, "spp_per_fb": a.spp, "max_depth": a.depth,
-                       "segments_per_step": int(segs), "parallelism": f"rows{world}"},
-            "roofline": roof,
-        }
+        workload = workload_name(a)
+        roof = roofline(a, stats, kname[0], avg_ms, len(rows), workload, world)
+        extra = {"cold_ms_per_step": round(dt_cold * 1e3, 3), "cold_value": round(segs / dt_cold / 1e6, 2),
+                 "cold_kernel_ms": round(cold_kms, 3), "kernel_ms": round(avg_ms, 3),
+                 "schedule": "steady state: every timed draw repeats the configuration and reuses the item "
+                             "schedule (and split-sample states) of the draws before it; cold_* = draws that "
+                             "reuse nothing (RT_FLAG_NO_SCHEDULE), as a single draw() runs",
+                 "timed_schedule_bits": sorted(set(sched)),
+                 "driver": "torch.distributed (one process per GPU)" if world > 1 else "single process"}
+        out = out_line(a, value, world, dt / a.steps, segs, roof, extra)
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a, a.cpu_seconds)
         print(json.dumps(out), flush=True)
@@ -322,6 +371,72 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_inprocess(a):
+    """`--gpus N` without a launcher: the product's C++ multi-GPU driver (librt_multi.so,
+    include/rt_multi.h) in this one process -- one rt_ctx per device on its own host thread, row
+    bands round-robin, ONE ncclGather of the 8-bit rows to rank 0 (RT_GATHER_RCCL, devices 0..N-1),
+    host assembly.  `--gather host` lets N ranks share the visible GPUs (a rehearsal of the tiling
+    on a one-GPU box; the rows are copied to the host instead of gathered over RCCL)."""
+    import torch
+
+    import raytracing_gpu_amd as rt
+    from raytracing_gpu_amd import multi
+
+    ndev = torch.cuda.device_count()
+    if a.gather == "rccl":
+        if ndev < a.gpus:
+            raise SystemExit(f"--gpus {a.gpus}: {ndev} visible devices (RCCL needs one device per rank; "
+                             "--gather host shares them)")
+        devices = list(range(a.gpus))
+        mode = multi.RT_GATHER_RCCL
+    else:
+        devices = [r % max(1, ndev) for r in range(a.gpus)]
+        mode = multi.RT_GATHER_HOST
+    m = multi.Multi(devices, mode)
+    sc = rt.Scene.builtin(a.scene, **scene_assets(a.scene)[0])
+    m.upload(sc)
+    cam = rt.RT_CAM_REF_SLOT0 if a.cam == "ref" else rt.RT_CAM_PER_PIXEL
+    kw = dict(band_rows=a.band_rows, exact=a.exact, lds=not a.no_lds, step=not a.no_step, bins=not a.no_bins)
+    args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, schedule=not a.no_schedule, **kw)
+    cold_args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, schedule=False, **kw)
+    m.draw(rt.make_args(64, 36, 1, 0, 1, a.depth, cam, band_rows=4))  # module load on every device
+    m.draw(cold_args)
+    colds = []
+    for _ in range(max(1, a.cold_steps)):
+        t0 = time.perf_counter()
+        _, cnt, tm = m.draw(cold_args)
+        colds.append((time.perf_counter() - t0, tm))
+    for _ in range(a.warmup):
+        m.draw(args)
+    warm = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):  # each draw is synchronous: every rank's stream and the gather drained
+        img, cnt, tm = m.draw(args)
+        warm.append(tm)
+    dt = time.perf_counter() - t0
+    segs = cnt["segments"]
+    value = segs * a.steps / dt / 1e6
+    dt_cold = sum(x[0] for x in colds) / len(colds)
+    per_rank_k = [round(sum(t["kernel_ms"][r] for t in warm) / len(warm), 3) for r in range(a.gpus)]
+    per_rank_cold = [round(sum(t[1]["kernel_ms"][r] for t in colds) / len(colds), 3) for r in range(a.gpus)]
+    extra = {"cold_ms_per_step": round(dt_cold * 1e3, 3), "cold_value": round(segs / dt_cold / 1e6, 2),
+             "kernel_ms_per_rank": per_rank_k, "cold_kernel_ms_per_rank": per_rank_cold,
+             "render_ms_max": round(sum(t["render_ms_max"] for t in warm) / len(warm), 3),
+             "gather_ms": round(sum(t["gather_ms"] for t in warm) / len(warm), 3),
+             "gather_bytes": warm[-1]["gather_bytes"], "warm": warm[-1]["warm"],
+             "schedule": "steady state: every timed draw repeats the configuration and reuses the item "
+                         "schedule (and split-sample states) of the draws before it; cold_* = draws that "
+                         "reuse nothing (RT_FLAG_NO_SCHEDULE), as a single draw() runs",
+             "driver": f"librt_multi.so in one process, {a.gpus} ranks on devices {devices}, "
+                       f"gather {'ncclGather (RCCL)' if mode == multi.RT_GATHER_RCCL else 'host copies'}; "
+                       "a step includes the copy of the assembled image to the host"}
+    out = out_line(a, value, a.gpus, dt / a.steps, segs, None, extra)
+    print(json.dumps(out), flush=True)
+    if a.png:
+        rt.write_png(a.png, img)
+    m.close()
 
 
 if __name__ == "__main__":

@@ -220,24 +220,34 @@ int rt_render_init(rt_ctx* ctx, int32_t width, int32_t height, uint64_t seed);
  * words the reference's render_init leaves in its state array). */
 int rt_read_states(rt_ctx* ctx, int64_t first, int64_t count, uint32_t* out);
 
-/* Renders fb ids [fb_first, fb_first+fb_count) for the owned rows into fb_dev (a DEVICE
- * pointer): layout [fb_count][owned_rows][width][3] floats, owned rows ascending.
+/* Renders fb ids [fb_first, fb_first+fb_count) for the owned rows into fb: layout
+ * [fb_count][owned_rows][width][3] floats, owned rows ascending.  fb may be a device (or managed)
+ * pointer, written by the kernel directly, or a host pointer (pinned or pageable): then the frame
+ * buffers are rendered into a temporary device buffer and copied back before the call returns.
  * counters may be NULL. */
-int rt_render(rt_ctx* ctx, const rt_render_args* args, float* fb_dev, rt_counters* counters);
+int rt_render(rt_ctx* ctx, const rt_render_args* args, float* fb, rt_counters* counters);
 /* Duration in ms of the last render kernel, from HIP events recorded on the context stream. */
 float rt_last_render_ms(const rt_ctx* ctx);
 /* Kernel of the last render launch as rocprof names it (stem, e.g. "render_step_kernel<25730>"):
  * the kernel variant the context picked for the scene's features and flags. */
 const char* rt_last_render_kernel(const rt_ctx* ctx);
+/* How the last render launch ordered its work (RT_SCHED_* bits; 0 = a cold launch: nothing from an
+ * earlier launch of the same configuration was used). */
+#define RT_SCHED_PREVIOUS 1     /* items claimed longest first by the segment counts of an earlier
+                                   launch of this configuration (same scene, size, spp, depth, fb
+                                   range, tiling and camera mode)                               */
+#define RT_SCHED_SPLIT_REPLAY 2 /* split samples started from RNG states an earlier launch recorded */
+int32_t rt_last_render_schedule(const rt_ctx* ctx);
 /* Audit log of the last RT_FLAG_AUDIT render: 16 floats per disagreeing BVH query (ray o[3] d[3]
  * time, tmin, tmax, culled t, culled prim (int bits), exact t, exact prim, culled rank, 0, 0).
  * Copies up to cap entries into out (may be NULL); returns the total number of disagreements. */
 int rt_audit_log(rt_ctx* ctx, float* out, int32_t cap);
 
 /* Quantise each fb (write_frame_buffer) and square-average them in fb order (average_images)
- * for the owned rows: out_dev = DEVICE pointer, [owned_rows][width][3] bytes, owned rows
- * ascending (row 0 of a PNG is image row height-1). */
-int rt_resolve(rt_ctx* ctx, const rt_render_args* args, const float* fb_dev, uint8_t* out_dev);
+ * for the owned rows: out = [owned_rows][width][3] bytes, owned rows ascending (row 0 of a PNG is
+ * image row height-1).  fb and out may each be a device or a host pointer (host buffers are
+ * staged through temporary device memory). */
+int rt_resolve(rt_ctx* ctx, const rt_render_args* args, const float* fb, uint8_t* out);
 
 /* draw(): init + render every fb + resolve, whole image, host output in PNG row order
  * (top row first), W*H*3 bytes.  counters may be NULL. */

@@ -36,8 +36,8 @@ typedef struct rt_multi_timing {
   float gather_bytes;                    /* bytes gathered to rank 0 (n_ranks * padded rows * W * 3) */
   float render_ms[RT_MULTI_MAX_RANKS];   /* per rank, host clock around its render_init..resolve     */
   float kernel_ms[RT_MULTI_MAX_RANKS];   /* per rank, render kernel alone (HIP events)               */
-  int32_t warm;                          /* 1: the ranks ran the longest-first item schedule recorded
-                                            by a previous draw of this configuration (rt_render)     */
+  int32_t warm;                          /* 1: every rank's launch reused the item schedule of an
+                                            earlier launch (rt_last_render_schedule & RT_SCHED_PREVIOUS) */
   int32_t pad;
 } rt_multi_timing;
 

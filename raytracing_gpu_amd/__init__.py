@@ -36,6 +36,8 @@ RT_FLAG_NO_STEP = 16
 RT_FLAG_NO_SCHEDULE = 32
 RT_FLAG_NO_CAMERA_BINS = 64
 RT_FLAG_NO_SPLIT = 128
+RT_SCHED_PREVIOUS = 1
+RT_SCHED_SPLIT_REPLAY = 2
 
 PRIM_SPHERE, PRIM_MOVING_SPHERE, PRIM_RECT_XY, PRIM_RECT_XZ, PRIM_RECT_YZ, PRIM_TRIANGLE = range(6)
 OBJ_PRIM, OBJ_LIST, OBJ_BVH, OBJ_XFORM, OBJ_MEDIUM = range(5)
@@ -113,6 +115,7 @@ ABI = {
     "rt_render": (c_int, [c_void_p, POINTER(rt_render_args), c_void_p, POINTER(rt_counters)]),
     "rt_last_render_ms": (c_float, [c_void_p]),
     "rt_last_render_kernel": (ctypes.c_char_p, [c_void_p]),
+    "rt_last_render_schedule": (c_int32, [c_void_p]),
     "rt_audit_log": (c_int, [c_void_p, POINTER(c_float), c_int32]),
     "rt_resolve": (c_int, [c_void_p, POINTER(rt_render_args), c_void_p, c_void_p]),
     "rt_draw": (c_int, [c_void_p, POINTER(rt_render_args), POINTER(c_uint8), POINTER(rt_counters)]),
@@ -321,6 +324,10 @@ class Context:
     def last_render_kernel(self) -> str:
         """rocprof name stem of the kernel the last render launched."""
         return lib().rt_last_render_kernel(self._c).decode()
+
+    def last_render_schedule(self) -> int:
+        """RT_SCHED_* bits of the last render launch (0: cold, nothing reused from an earlier launch)."""
+        return int(lib().rt_last_render_schedule(self._c))
 
     def audit_log(self, cap: int = 4096) -> tuple[int, np.ndarray]:
         """(number of disagreements, [min(n, cap), 16] float32 entries) of the last audit render."""

@@ -2146,8 +2146,9 @@ struct rt_ctx {
   uint16_t* item_cost = nullptr;
   uint32_t* perm = nullptr;
   long long item_cap = 0;
-  long long perm_key[10] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
-  long long pending_key[10] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1};  // measured, schedule not built yet
+  static constexpr int kKey = 11;
+  long long perm_key[kKey] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+  long long pending_key[kKey] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};  // measured, schedule not built yet
   unsigned long long pending_segs = 0;
   unsigned long long n_long = 0;
   // Split samples of the longest items (render_step_kernel; see rt_render): n_split perm positions,
@@ -2169,6 +2170,7 @@ struct rt_ctx {
   bool world_step = false;  // one BVH object followed by primitive objects (render_step_kernel applies)
   int dev_nodes = 0, dev_prims = 0, dev_mats = 0, dev_texs = 0;  // device array sizes (for LDS staging)
   float last_ms = 0.0f;
+  int last_sched = 0;  // RT_SCHED_* of the last render launch
   char last_kernel[48] = "";  // rocprof name stem of the last render launch, e.g. render_step_kernel<25730>
   float* dbg = nullptr;  // audit log: [0] = count, then 16 floats per entry
   // Camera-ray candidate lists (world = one BVH): bounding spheres of the world BVH's primitives
@@ -2951,24 +2953,27 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   // bucket), and waves holding one of the top ~2 % run at raised priority.  A lane runs an item's samples serially, so
   // an item that starts late under full load (22 us per segment per lane on C2) decides when a
   // small share (a rank of a multi-GPU run) ends.  Pixel results do not depend on the order.
-  const long long pkey[10] = {c->scene_gen, a->width, a->height, a->spp, a->max_depth,
-                              a->fb_first, a->fb_count, a->band_rows, a->band_first, a->band_stride};
+  // cam_mode is part of the key: the split samples' recorded sample-start states depend on it (the
+  // PER_PIXEL camera draws come from the pixel's own state, REF ones from the slot-0 copy)
+  constexpr int K = rt_ctx::kKey;
+  const long long pkey[K] = {c->scene_gen, a->width,   a->height,    a->spp,       a->max_depth, a->fb_first,
+                             a->fb_count,  a->band_rows, a->band_first, a->band_stride, a->cam_mode};
   const bool sched = items <= (64LL << 20) && (a->flags & RT_FLAG_NO_SCHEDULE) == 0;
-  if (sched && !std::equal(pkey, pkey + 10, c->perm_key) && std::equal(pkey, pkey + 10, c->pending_key) &&
+  if (sched && !std::equal(pkey, pkey + K, c->perm_key) && std::equal(pkey, pkey + K, c->pending_key) &&
       items <= c->item_cap) {  // the configuration repeats: its schedule from the measured counts
     if ((rc = build_schedule(c, items, a->spp, c->pending_segs))) return rc;
-    std::copy(pkey, pkey + 10, c->perm_key);
-    std::fill(c->pending_key, c->pending_key + 10, -1LL);
+    std::copy(pkey, pkey + K, c->perm_key);
+    std::fill(c->pending_key, c->pending_key + K, -1LL);
   }
-  const bool have_perm = sched && std::equal(pkey, pkey + 10, c->perm_key);
+  const bool have_perm = sched && std::equal(pkey, pkey + K, c->perm_key);
   if (sched && items > c->item_cap) {
     if (c->item_cost) HIPCHK(c, hipFree(c->item_cost));
     if (c->perm) HIPCHK(c, hipFree(c->perm));
     c->item_cost = nullptr;
     c->perm = nullptr;
     c->item_cap = 0;
-    std::fill(c->perm_key, c->perm_key + 10, -1LL);
-    std::fill(c->pending_key, c->pending_key + 10, -1LL);
+    std::fill(c->perm_key, c->perm_key + K, -1LL);
+    std::fill(c->pending_key, c->pending_key + K, -1LL);
     HIPCHK(c, hipMalloc((void**)&c->item_cost, (size_t)items * sizeof(uint16_t)));
     HIPCHK(c, hipMalloc((void**)&c->perm, (size_t)items * sizeof(uint32_t)));
     c->item_cap = items;
@@ -3206,6 +3211,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  c->last_sched = (have_perm ? RT_SCHED_PREVIOUS : 0) | (split_mode == 2 ? RT_SCHED_SPLIT_REPLAY : 0);
   snprintf(c->last_kernel, sizeof(c->last_kernel), "%s<%d>",
            (kVariants[var].mask & F_STEP) != 0 ? "render_step_kernel" : "render_kernel", kVariants[var].mask);
   unsigned long long host_cnt[8];
@@ -3221,7 +3227,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     for (int q = 0; q < rows; ++q) c->host_cost[rm[q]] = cost[rm[q]];
   }
   if (sched && !have_perm) {  // the schedule is built from these counts when the configuration repeats
-    std::copy(pkey, pkey + 10, c->pending_key);
+    std::copy(pkey, pkey + K, c->pending_key);
     c->pending_segs = host_cnt[1];
   }
   if (split_mode == 1) {  // sample-start states recorded for this seed
@@ -3281,6 +3287,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
 
 float rt_last_render_ms(const rt_ctx* c) { return c ? c->last_ms : 0.0f; }
 const char* rt_last_render_kernel(const rt_ctx* c) { return c ? c->last_kernel : ""; }
+int32_t rt_last_render_schedule(const rt_ctx* c) { return c ? c->last_sched : 0; }
 
 int rt_read_states(rt_ctx* c, int64_t first, int64_t count, uint32_t* out) {
   if (!c || !out || first < 0 || count < 0) return fail(c, RT_ERR_ARG, "bad read_states args");

@@ -33,7 +33,7 @@ struct rt_multi {
   uint8_t* gathered = nullptr;   // rank 0: n * padded bytes
   size_t gathered_cap = 0;
   std::vector<uint8_t> host;     // host copy of the gathered rows
-  long long last_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  bool broken = false;  // a collective failed: the communicator is not reused
   std::string err;
 };
 
@@ -136,7 +136,6 @@ int rt_multi_upload(rt_multi* m, const rt_scene_soa* scene) {
     const int rc = rt_scene_upload(m->ctx[r], scene);
     if (rc != RT_OK) return fail(m, rc, std::string("rank ") + std::to_string(r) + ": " + rt_last_error(m->ctx[r]));
   }
-  std::fill(m->last_key, m->last_key + 8, -1LL);  // a new scene: the next draw runs cold
   return RT_OK;
 }
 
@@ -169,16 +168,13 @@ int rt_multi_draw(rt_multi* m, const rt_render_args* args, uint8_t* png_rgb_host
     int rc = grow(m, m->dev[0], (void**)&m->gathered, &m->gathered_cap, padded * n);
     if (rc) return rc;
   }
-  // warm = this configuration was drawn before (rt_render keeps its item schedule per context)
-  const long long key[8] = {args->width, args->height, args->spp, args->fb_count, args->max_depth,
-                            args->band_rows, args->flags, (long long)args->seed};
-  const bool warm = std::equal(key, key + 8, m->last_key);
 
   // ---- every rank: render_init + render + resolve of its rows, on its own host thread
   std::vector<int> status(n, RT_OK);
   std::vector<rt_counters> cnt(n);
   std::vector<double> rms(n, 0.0);
   std::vector<float> kms(n, 0.0f);
+  std::vector<int> sched(n, 0);  // rt_last_render_schedule of each rank's launch
   std::vector<std::thread> th;
   for (int r = 0; r < n; ++r) {
     th.emplace_back([&, r]() {
@@ -187,7 +183,10 @@ int rt_multi_draw(rt_multi* m, const rt_render_args* args, uint8_t* png_rgb_host
       if (rows[r].empty()) return;
       int rc = rt_render_init(c, W, H, args->seed);
       if (!rc) rc = rt_render(c, &ra[r], m->fb[r], &cnt[r]);
-      if (!rc) kms[r] = rt_last_render_ms(c);
+      if (!rc) {
+        kms[r] = rt_last_render_ms(c);
+        sched[r] = rt_last_render_schedule(c);
+      }
       if (!rc) rc = rt_resolve(c, &ra[r], m->fb[r], m->rows8[r]);
       status[r] = rc;
       rms[r] = now_ms() - a;
@@ -202,17 +201,27 @@ int rt_multi_draw(rt_multi* m, const rt_render_args* args, uint8_t* png_rgb_host
   const double g0 = now_ms();
   m->host.resize(padded * n);
   if (m->mode == RT_GATHER_RCCL) {
+    if (m->broken) return fail(m, RT_ERR_STATE, "an earlier collective failed: destroy this rt_multi");
     if (ncclGroupStart() != ncclSuccess) return fail(m, RT_ERR_HIP, "ncclGroupStart");
-    for (int r = 0; r < n; ++r) {
+    // the group is always closed, whatever fails inside it: a thread left inside an open RCCL group
+    // would fold its next collectives into this one
+    int gerr = -1;
+    for (int r = 0; r < n && gerr < 0; ++r) {
       (void)hipSetDevice(m->dev[r]);
       if (ncclGather(m->rows8[r], r == 0 ? m->gathered : nullptr, padded, ncclUint8, 0, m->comm[r], m->stream[r]) !=
           ncclSuccess)
-        return fail(m, RT_ERR_HIP, "ncclGather");
+        gerr = r;
     }
-    if (ncclGroupEnd() != ncclSuccess) return fail(m, RT_ERR_HIP, "ncclGroupEnd");
-    for (int r = 0; r < n; ++r) {
+    const bool end_ok = ncclGroupEnd() == ncclSuccess;
+    bool sync_ok = true;
+    for (int r = 0; r < n; ++r) {  // every rank's stream drained, also after a failure
       (void)hipSetDevice(m->dev[r]);
-      if (hipStreamSynchronize(m->stream[r]) != hipSuccess) return fail(m, RT_ERR_HIP, "gather sync");
+      if (hipStreamSynchronize(m->stream[r]) != hipSuccess) sync_ok = false;
+    }
+    if (gerr >= 0 || !end_ok || !sync_ok) {
+      m->broken = true;  // the communicator's state is unknown after a failed collective
+      return fail(m, RT_ERR_HIP, gerr >= 0 ? "ncclGather (rank " + std::to_string(gerr) + ")"
+                                           : (!end_ok ? "ncclGroupEnd" : "gather sync"));
     }
     (void)hipSetDevice(m->dev[0]);
     if (hipMemcpy(m->host.data(), m->gathered, padded * n, hipMemcpyDeviceToHost) != hipSuccess)
@@ -253,9 +262,11 @@ int rt_multi_draw(rt_multi* m, const rt_render_args* args, uint8_t* png_rgb_host
     timing->gather_ms = (float)(g1 - g0);
     timing->gather_bytes = (float)(padded * n);
     timing->total_ms = (float)(now_ms() - t0);
-    timing->warm = warm ? 1 : 0;
+    int warm = 1;
+    for (int r = 0; r < n; ++r)
+      if (!rows[r].empty() && (sched[r] & RT_SCHED_PREVIOUS) == 0) warm = 0;
+    timing->warm = warm;
   }
-  std::copy(key, key + 8, m->last_key);
   return RT_OK;
 }
 

@@ -513,3 +513,72 @@ def test_full_size_mesh_rows(rtlib, gpu_ctx, oracle, scene, W, H, spp, rows):
     for f in range(nfb):
         want = ref.render(W, H, spp, f, 50, REF, rows=rows)[0].reshape(H, W, 3)
         assert np.array_equal(_bits(got[f][js]), _bits(want[js])), f"{scene} fb {f}"
+
+
+def test_split_samples_switch_cam_mode_and_seed(rtlib, gpu_ctx, oracle):
+    """One context, one configuration drawn warm in REF mode (measure, record, split), then with
+    the other camera mode and another seed in between: the split items must never start from RNG
+    states recorded under another camera mode or seed.  Every launch equals the oracle (seed 1984)
+    or the cold render of the same seed (seed 7), bit for bit."""
+    import torch
+
+    W, H, spp, nfb = 96, 54, 4, 2
+    gpu_ctx.upload(rtlib.Scene.builtin("big1"))
+    ref = oracle.RefScene("big1")
+    want = {cam: [ref.render(W, H, spp, f, 50, cam)[0].reshape(H, W, 3) for f in range(nfb)] for cam in (REF, PIX)}
+
+    def launch(cam, seed=1984, **kw):
+        gpu_ctx.render_init(W, H, seed)
+        fb = torch.full((nfb * H * W * 3,), float("nan"), dtype=torch.float32, device="cuda")
+        cnt = gpu_ctx.render(rtlib.make_args(W, H, spp, 0, nfb, 50, cam, seed=seed, **kw), fb.data_ptr())
+        return fb.cpu().numpy().reshape(nfb, H, W, 3), cnt, gpu_ctx.last_render_schedule()
+
+    cold7 = {cam: launch(cam, 7, schedule=False)[0] for cam in (REF, PIX)}
+    seen = set()
+    for k, (cam, seed) in enumerate([(REF, 1984)] * 4 + [(PIX, 1984), (REF, 1984), (PIX, 1984), (PIX, 1984),
+                                     (PIX, 1984), (REF, 7), (REF, 1984), (PIX, 7), (PIX, 1984)]):
+        got, cnt, sched = launch(cam, seed)
+        seen.add(sched)
+        exp = want[cam] if seed == 1984 else cold7[cam]
+        for f in range(nfb):
+            assert np.array_equal(_bits(got[f]), _bits(exp[f])), f"launch {k} cam {cam} seed {seed} fb {f}"
+        assert cnt["samples"] == nfb * H * W * spp
+    assert rtlib.RT_SCHED_PREVIOUS | rtlib.RT_SCHED_SPLIT_REPLAY in seen  # the split replay did run
+
+
+@pytest.mark.parametrize("launches", [4])
+def test_c2_primary_split_rows(rtlib, gpu_ctx, oracle, launches):
+    """C2 as SURVEY.md 8d names it first: no_fb = 1 x samples_per_pixel_per_fb = 100 (render.h:24's
+    default), 1200x800, depth 50.  Every launch of the whole image (cold, schedule, split-recording,
+    split-replay) against the oracle on a row subset."""
+    import torch
+
+    W, H, spp = 1200, 800, 100
+    rows = (3, 101)  # 8 rows
+    js = list(range(rows[0], H, rows[1]))
+    want = oracle.RefScene("big1").render(W, H, spp, 0, 50, REF, rows=rows)[0].reshape(H, W, 3)
+    gpu_ctx.upload(rtlib.Scene.builtin("big1"))
+    args = rtlib.make_args(W, H, spp, 0, 1, 50, REF)
+    for launch in range(launches):
+        gpu_ctx.render_init(W, H, 1984)
+        fb = torch.full((H * W * 3,), float("nan"), dtype=torch.float32, device="cuda")
+        cnt = gpu_ctx.render(args, fb.data_ptr())
+        got = fb.cpu().numpy().reshape(H, W, 3)
+        assert np.array_equal(_bits(got[js]), _bits(want[js])), f"launch {launch}"
+        assert not np.isnan(got).any()
+        assert cnt["samples"] == W * H * spp
+
+
+def test_c2_primary_split_culled_equals_exact(rtlib, gpu_ctx):
+    """The whole 1 x 100 C2 workload: culled (and, from the third launch, split-sample) rendering
+    equals the reference visit set, every float, same segment count."""
+    ex, _, ce, _, _ = _gpu_render(rtlib, gpu_ctx, "big1", 1200, 800, 100, 0, 1, REF, exact=True)
+    import torch
+
+    args = rtlib.make_args(1200, 800, 100, 0, 1, 50, REF)
+    for launch in range(3):
+        gpu_ctx.render_init(1200, 800, 1984)
+        fb = torch.zeros(1200 * 800 * 3, dtype=torch.float32, device="cuda")
+        cf = gpu_ctx.render(args, fb.data_ptr())
+        assert cf["segments"] == ce["segments"], f"launch {launch}"
+        assert np.array_equal(_bits(fb.cpu().numpy().reshape(ex.shape)), _bits(ex)), f"launch {launch}"
