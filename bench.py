@@ -325,6 +325,7 @@ def main():
     dt_cold = timed(max(1, a.cold_steps), cold_args) / max(1, a.cold_steps)
     cold_kms = sum(kms) / len(kms)
     assert all(x == 0 for x in sched), sched
+    cold_sched = sorted(set(sched))
 
     stats = None
     if not a.no_stats:  # untimed pass of the counting variant: node / prim tests for B_seg
@@ -357,7 +358,7 @@ def main():
                  "schedule": "steady state: every timed draw repeats the configuration and reuses the item "
                              "schedule (and split-sample states) of the draws before it; cold_* = draws that "
                              "reuse nothing (RT_FLAG_NO_SCHEDULE), as a single draw() runs",
-                 "timed_schedule_bits": sorted(set(sched)),
+                 "timed_schedule_bits": sorted(set(sched)), "cold_schedule_bits": cold_sched,
                  "driver": "torch.distributed (one process per GPU)" if world > 1 else "single process"}
         out = out_line(a, value, world, dt / a.steps, segs, roof, extra)
         if world == 1 and not a.no_cpu_baseline:

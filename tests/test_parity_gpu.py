@@ -418,6 +418,33 @@ def test_bench_two_ranks_match_one(tmp_path):
     assert (tmp_path / "n1.png").read_bytes() == (tmp_path / "n2.png").read_bytes()
 
 
+def test_bench_inprocess_two_ranks_match_one(tmp_path):
+    """`python bench.py --gpus 2` exactly as the driver invokes BENCH (no launcher): the C++
+    multi-GPU driver (librt_multi.so) in one process, two ranks sharing the box's GPU with host
+    gathers.  The JSON line says n_gpus 2 and the assembled image is byte-identical to N = 1."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["bench.py", "--steps", "1", "--warmup", "1", "--cold-steps", "1", "--no-cpu-baseline",
+              "--no-stats", "--width", "200", "--height", "112", "--spp", "2", "--nfb", "2"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    one = subprocess.run([sys.executable, *common, "--png", str(tmp_path / "n1.png")], cwd=root, env=env,
+                         capture_output=True, text=True, timeout=600)
+    assert one.returncode == 0, one.stderr[-2000:]
+    two = subprocess.run([sys.executable, *common, "--gpus", "2", "--gather", "host",
+                          "--png", str(tmp_path / "n2.png")], cwd=root, env=env,
+                         capture_output=True, text=True, timeout=600)
+    assert two.returncode == 0, two.stderr[-2000:]
+    line = json.loads([x for x in two.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and "librt_multi.so" in line["driver"]
+    assert line["value"] > 0 and line["cold_ms_per_step"] > 0
+    assert (tmp_path / "n1.png").read_bytes() == (tmp_path / "n2.png").read_bytes()
+
+
 def test_host_buffers_match_device(rtlib, gpu_ctx, oracle):
     """rt_render / rt_resolve also take host pointers (host or device frame buffer):
     the kernels write a staged device buffer that is copied back; bits equal the device path's
@@ -582,3 +609,4 @@ def test_c2_primary_split_culled_equals_exact(rtlib, gpu_ctx):
         cf = gpu_ctx.render(args, fb.data_ptr())
         assert cf["segments"] == ce["segments"], f"launch {launch}"
         assert np.array_equal(_bits(fb.cpu().numpy().reshape(ex.shape)), _bits(ex)), f"launch {launch}"
+
