@@ -2539,7 +2539,13 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
     // lanes of the stepwise kernel that runs the split launches (4 waves/SIMD: 1024 per CU),
     // whatever variant measured (bench.py measures with the counting variant)
     const double lanes = (double)c->cus * 1024.0;
-    double thr = (double)items < 6.0 * lanes ? 24.0 : std::max(32.0, 0.5 * (double)segs / lanes);
+    // Long items (spp > 16, e.g. C2's primary 1 x 100 split) are split only above a third of a
+    // lane's share: splitting them all turns the launch into one refill per sample (C2 1 x 100,
+    // N = 1 warm: every item split 24.9 ms; above 300 segments 19.4, 400: 20.9, 600: 25.4 ms; the
+    // N = 8 share (117 segments per lane) needs <= 100: 3.2 ms, 300: 8.2 ms).
+    const double share = (double)segs / lanes;
+    double thr = (double)items >= 6.0 * lanes ? std::max(32.0, 0.5 * share)
+                                               : (spp <= 16 ? 24.0 : std::max(24.0, 0.33 * share));
     if (const char* e = getenv("RT_SPLIT_MIN_SEGMENTS")) thr = atof(e);  // tuning
     const long long bt = (long long)std::ceil(thr / (double)(1 << shift));
     long long ns = 0;
@@ -3043,6 +3049,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   const bool step = c->world_step && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
   const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
                                (a->flags & RT_FLAG_WIDEST) != 0, step);
+  if (var < 0) return fail(c, RT_ERR_SCENE, "no kernel variant covers the scene features");
   // shading phase of render_step_kernel once this many lanes of a wave wait (RT_SHADE_MIN: tuning)
   // (measured: C2 best at 60 of 64 lanes; C4's triangle-mesh steps at 48: 125.0 -> 119.7 ms, 40: 121.8)
   P.shade_min = (kVariants[var].mask & F_TRI) != 0 ? kShadeMinMesh : kShadeMin;
@@ -3107,7 +3114,6 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     P.S.dbg_n = (unsigned*)c->dbg;
     P.S.dbg_cap = kAuditCap;
   }
-  if (var < 0) return fail(c, RT_ERR_SCENE, "no kernel variant covers the scene features");
   const int bs = variant_block(var);
   const bool lds_var = (kVariants[var].mask & F_LDS) != 0;
   P.S.lds_nodes = lds_var ? c->dev_nodes : 0;
