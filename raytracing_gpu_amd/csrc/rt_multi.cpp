@@ -1,6 +1,7 @@
 // rt_multi.cpp — multi-GPU draw() over one node (include/rt_multi.h): one rt_ctx per rank, row
-// bands dealt round-robin, each rank renders + resolves its rows on its own host thread, one RCCL
-// gather of the 8-bit rows to rank 0 over xGMI, host assembly in PNG row order.
+// bands dealt round-robin, each rank renders + resolves its rows on its own persistent host thread,
+// one RCCL gather of the 8-bit rows to rank 0 over xGMI, one DMA copy into pinned host memory, and
+// the ranks' threads assemble the image in PNG row order.
 //
 // Replaces render.h:118-174 (draw) for a frame buffer tiled across GPUs.  The
 // reference has no multi-GPU path; its per-pixel independence (RNG slot ((id+1)p+id+1) mod N and
@@ -11,8 +12,11 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -32,9 +36,19 @@ struct rt_multi {
   std::vector<size_t> fb_cap, rows_cap;
   uint8_t* gathered = nullptr;   // rank 0: n * padded bytes
   size_t gathered_cap = 0;
-  std::vector<uint8_t> host;     // host copy of the gathered rows
+  uint8_t* host = nullptr;       // pinned host copy of the gathered rows (DMA, not a staged copy)
+  size_t host_cap = 0;
   bool broken = false;  // a collective failed: the communicator is not reused
   std::string err;
+  // One persistent host thread per rank (its device set once): a draw posts one job per phase
+  // instead of creating threads.
+  std::vector<std::thread> workers;
+  std::mutex mu;
+  std::condition_variable go, done;
+  std::function<void(int)> job;
+  unsigned long long gen = 0;
+  int pending = 0;
+  bool quit = false;
 };
 
 namespace {
@@ -46,6 +60,34 @@ int fail(rt_multi* m, int code, const std::string& msg) {
 
 double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Runs job(r) on every rank's thread and waits for all of them.
+void run_ranks(rt_multi* m, std::function<void(int)> job) {
+  std::unique_lock<std::mutex> lk(m->mu);
+  m->job = std::move(job);
+  m->pending = m->n;
+  ++m->gen;
+  m->go.notify_all();
+  m->done.wait(lk, [m] { return m->pending == 0; });
+}
+
+void worker(rt_multi* m, int r) {
+  (void)hipSetDevice(m->dev[r]);
+  unsigned long long seen = 0;
+  for (;;) {
+    std::function<void(int)> job;
+    {
+      std::unique_lock<std::mutex> lk(m->mu);
+      m->go.wait(lk, [&] { return m->quit || m->gen != seen; });
+      if (m->quit) return;
+      seen = m->gen;
+      job = m->job;
+    }
+    job(r);
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (--m->pending == 0) m->done.notify_one();
+  }
 }
 
 // grow a device buffer on `dev`
@@ -105,12 +147,20 @@ int rt_multi_create(int32_t n_ranks, const int32_t* devices, int32_t gather_mode
       return RT_ERR_HIP;
     }
   }
+  for (int r = 0; r < n_ranks; ++r) m->workers.emplace_back(worker, m, r);
   *out = m;
   return RT_OK;
 }
 
 int rt_multi_destroy(rt_multi* m) {
   if (!m) return RT_ERR_ARG;
+  {
+    std::lock_guard<std::mutex> lk(m->mu);
+    m->quit = true;
+    m->go.notify_all();
+  }
+  for (std::thread& t : m->workers) t.join();
+  if (m->host) (void)hipHostFree(m->host);
   for (ncclComm_t c : m->comm)
     if (c) ncclCommDestroy(c);
   for (int r = 0; r < m->n; ++r) {
@@ -169,37 +219,45 @@ int rt_multi_draw(rt_multi* m, const rt_render_args* args, uint8_t* png_rgb_host
     if (rc) return rc;
   }
 
-  // ---- every rank: render_init + render + resolve of its rows, on its own host thread
+  if (padded * n > m->host_cap) {
+    if (m->host) (void)hipHostFree(m->host);
+    m->host = nullptr;
+    m->host_cap = 0;
+    if (hipHostMalloc((void**)&m->host, padded * n, hipHostMallocDefault) != hipSuccess)
+      return fail(m, RT_ERR_NOMEM, "hipHostMalloc in rt_multi");
+    m->host_cap = padded * n;
+  }
+
+  // ---- every rank: render_init + render + resolve of its rows, on its own host thread (host
+  // gather: its rows copied into the pinned buffer too)
   std::vector<int> status(n, RT_OK);
   std::vector<rt_counters> cnt(n);
   std::vector<double> rms(n, 0.0);
   std::vector<float> kms(n, 0.0f);
   std::vector<int> sched(n, 0);  // rt_last_render_schedule of each rank's launch
-  std::vector<std::thread> th;
-  for (int r = 0; r < n; ++r) {
-    th.emplace_back([&, r]() {
-      const double a = now_ms();
-      rt_ctx* c = m->ctx[r];
-      if (rows[r].empty()) return;
-      int rc = rt_render_init(c, W, H, args->seed);
-      if (!rc) rc = rt_render(c, &ra[r], m->fb[r], &cnt[r]);
-      if (!rc) {
-        kms[r] = rt_last_render_ms(c);
-        sched[r] = rt_last_render_schedule(c);
-      }
-      if (!rc) rc = rt_resolve(c, &ra[r], m->fb[r], m->rows8[r]);
-      status[r] = rc;
-      rms[r] = now_ms() - a;
-    });
-  }
-  for (auto& t : th) t.join();
+  run_ranks(m, [&](int r) {
+    const double a = now_ms();
+    rt_ctx* c = m->ctx[r];
+    if (rows[r].empty()) return;
+    int rc = rt_render_init(c, W, H, args->seed);
+    if (!rc) rc = rt_render(c, &ra[r], m->fb[r], &cnt[r]);
+    if (!rc) {
+      kms[r] = rt_last_render_ms(c);
+      sched[r] = rt_last_render_schedule(c);
+    }
+    if (!rc) rc = rt_resolve(c, &ra[r], m->fb[r], m->rows8[r]);
+    if (!rc && m->mode == RT_GATHER_HOST &&
+        hipMemcpy(m->host + padded * r, m->rows8[r], rows[r].size() * W * 3, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = RT_ERR_HIP;
+    status[r] = rc;
+    rms[r] = now_ms() - a;
+  });
   for (int r = 0; r < n; ++r)
     if (status[r] != RT_OK)
       return fail(m, status[r], std::string("rank ") + std::to_string(r) + ": " + rt_last_error(m->ctx[r]));
 
   // ---- one gather of the padded 8-bit rows to rank 0
   const double g0 = now_ms();
-  m->host.resize(padded * n);
   if (m->mode == RT_GATHER_RCCL) {
     if (m->broken) return fail(m, RT_ERR_STATE, "an earlier collective failed: destroy this rt_multi");
     if (ncclGroupStart() != ncclSuccess) return fail(m, RT_ERR_HIP, "ncclGroupStart");
@@ -224,22 +282,15 @@ int rt_multi_draw(rt_multi* m, const rt_render_args* args, uint8_t* png_rgb_host
                                            : (!end_ok ? "ncclGroupEnd" : "gather sync"));
     }
     (void)hipSetDevice(m->dev[0]);
-    if (hipMemcpy(m->host.data(), m->gathered, padded * n, hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipMemcpy(m->host, m->gathered, padded * n, hipMemcpyDeviceToHost) != hipSuccess)
       return fail(m, RT_ERR_HIP, "copy gathered rows");
-  } else {
-    for (int r = 0; r < n; ++r) {
-      if (rows[r].empty()) continue;
-      (void)hipSetDevice(m->dev[r]);
-      if (hipMemcpy(m->host.data() + padded * r, m->rows8[r], rows[r].size() * W * 3, hipMemcpyDeviceToHost) !=
-          hipSuccess)
-        return fail(m, RT_ERR_HIP, "copy rank rows");
-    }
   }
-  // ---- assembly: owned row j (0 = bottom) goes to PNG row H-1-j
+  // ---- assembly: owned row j (0 = bottom) goes to PNG row H-1-j; each rank's thread copies its rows
   const size_t rowb = (size_t)W * 3;
-  for (int r = 0; r < n; ++r)
+  run_ranks(m, [&](int r) {
     for (size_t q = 0; q < rows[r].size(); ++q)
-      memcpy(png_rgb_host + (size_t)(H - 1 - rows[r][q]) * rowb, m->host.data() + padded * r + q * rowb, rowb);
+      memcpy(png_rgb_host + (size_t)(H - 1 - rows[r][q]) * rowb, m->host + padded * r + q * rowb, rowb);
+  });
   const double g1 = now_ms();
 
   if (counters) {

@@ -16,7 +16,7 @@ import numpy as np
 from . import lib as _rt_lib
 from . import rt_counters, rt_render_args, rt_scene_soa, RtError
 
-MULTI_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "librt_multi.so")
+MULTI_PATH = os.environ.get("RT_MULTI_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "librt_multi.so")  # override: experiments
 RT_GATHER_RCCL = 0
 RT_GATHER_HOST = 1
 MAX_RANKS = 16
