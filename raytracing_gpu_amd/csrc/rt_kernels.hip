@@ -820,15 +820,26 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
   }
   const float2 pm = pmargin_of<F>(S)[best_prim];
   const unsigned must = bound < pm.y ? __float_as_uint(pm.x) : 0xffffffffu;
-  const V inv = inv_of();
+  // The remaining positions: an ancestor whose box holds the computed hit point deeper than
+  // `bound` cannot reject the ray either (the same argument as for the winner's own box, on the
+  // actual hit point instead of the primitive's box: triangles and rects touch their boxes along
+  // whole faces, but a hit point rarely lies near an ancestor's faces); the others get the
+  // reference's slab test, with its IEEE reciprocals.
+  const V p = r.o + best * r.d;
   int pos = 0;
   for (int kr = last0 + (best_rank >> 1);; kr = (kr - 1) >> 1, ++pos) {
     if ((must >> pos) & 1u) {
       if constexpr ((F & F_STATS) != 0) ++nnode;
       const float4 lo = nodes_of<F>(S)[2 * (base + kr)], hi = nodes_of<F>(S)[2 * (base + kr) + 1];
-      if (!box_hit(lo, hi, r, inv, tmin, tmax)) {
-        if constexpr ((F & F_STATS) != 0) ++nfall;
-        return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
+      const float mx = __builtin_fminf(p.x - lo.x, hi.x - p.x);
+      const float my = __builtin_fminf(p.y - lo.y, hi.y - p.y);
+      const float mz = __builtin_fminf(p.z - lo.z, hi.z - p.z);
+      if (!(__builtin_fminf(__builtin_fminf(mx, my), mz) > bound)) {
+        const V inv = inv_of();  // rare: not kept live across the chain
+        if (!box_hit(lo, hi, r, inv, tmin, tmax)) {
+          if constexpr ((F & F_STATS) != 0) ++nfall;
+          return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
+        }
       }
     }
     if (kr == 0) return true;
