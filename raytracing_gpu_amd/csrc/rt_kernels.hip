@@ -825,7 +825,12 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
   // actual hit point instead of the primitive's box: triangles and rects touch their boxes along
   // whole faces, but a hit point rarely lies near an ancestor's faces); the others get the
   // reference's slab test, with its IEEE reciprocals.
+  // Margin needed here: the reference's slab values (lo - o) * RN(1/d) carry ~3 roundings of
+  // |lo - o| <= |lo| + |o| in distance terms, and p = o + t d (our float evaluation at the
+  // reference's own t) is within a few ulp of |o| + t |d|: 2^-20 of their sum is > 4x both.
   const V p = r.o + best * r.d;
+  const float obase = 2.0f * (__builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.o.x), __builtin_fabsf(r.o.y)),
+                                              __builtin_fabsf(r.o.z)) + best * dmax);
   int pos = 0;
   for (int kr = last0 + (best_rank >> 1);; kr = (kr - 1) >> 1, ++pos) {
     if ((must >> pos) & 1u) {
@@ -834,7 +839,11 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
       const float mx = __builtin_fminf(p.x - lo.x, hi.x - p.x);
       const float my = __builtin_fminf(p.y - lo.y, hi.y - p.y);
       const float mz = __builtin_fminf(p.z - lo.z, hi.z - p.z);
-      if (!(__builtin_fminf(__builtin_fminf(mx, my), mz) > bound)) {
+      const float bmax = __builtin_fmaxf(
+          __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(lo.x), __builtin_fabsf(lo.y)), __builtin_fabsf(lo.z)),
+          __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(hi.x), __builtin_fabsf(hi.y)), __builtin_fabsf(hi.z)));
+      const float need = 0x1p-20f * (bmax + obase);
+      if (!(__builtin_fminf(__builtin_fminf(mx, my), mz) > need)) {
         const V inv = inv_of();  // rare: not kept live across the chain
         if (!box_hit(lo, hi, r, inv, tmin, tmax)) {
           if constexpr ((F & F_STATS) != 0) ++nfall;
@@ -1427,7 +1436,12 @@ constexpr int render_wpe() {
   return (F & F_LDS) != 0 ? 1 : RT_WPE_GLOBAL;
 #else
   constexpr int feat = F & F_ALL;
-  return (F & F_LDS) != 0 ? 1 : ((feat == F_CORNELL || feat == F_FINAL || feat == F_MESH) ? 4 : (feat == F_ALL ? 3 : 1));
+#ifndef RT_WPE_FINAL
+#define RT_WPE_FINAL 4
+#endif
+  return (F & F_LDS) != 0 ? 1
+                          : (feat == F_FINAL ? RT_WPE_FINAL
+                                             : ((feat == F_CORNELL || feat == F_MESH) ? 4 : (feat == F_ALL ? 3 : 1)));
 #endif
 }
 template <int F>

@@ -265,6 +265,8 @@ def test_culled_equals_exact_full_workload(rtlib, gpu_ctx, scene, W, H, spp, nfb
 @pytest.mark.parametrize("scene,W,H,spp,nfb", [
     ("final", 640, 360, 4, 2),            # C5 composition: ground boxes, xformed BVHs, media, door mesh
     ("door", 480, 270, 4, 2),             # C4 geometry (the real door mesh)
+    ("door", 1920, 1079, 2, 1),           # C4 at its full image size
+    ("final", 1280, 720, 2, 1),           # C5's bench size
 ])
 def test_culled_equals_exact_asset_scenes(rtlib, gpu_ctx, scene, W, H, spp, nfb):
     """Mesh / texture scenes at sizes past the oracle's reach: culled traversal (candidate ranges,
