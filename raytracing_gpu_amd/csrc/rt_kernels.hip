@@ -815,7 +815,16 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
       const float mx = __builtin_fminf(p.x - (c.x - rad), (c.x + rad) - p.x);
       const float my = __builtin_fminf(p.y - (c.y - rad), (c.y + rad) - p.y);
       const float mz = __builtin_fminf(p.z - (c.z - rad), (c.z + rad) - p.z);
-      if (__builtin_fminf(__builtin_fminf(mx, my), mz) > bound) return true;
+      // the chain check's per-ancestor margin below, taken at its largest: the root box's magnitude
+      const float4 rlo = S.nodes[2 * base], rhi = S.nodes[2 * base + 1];
+      const float rmax = __builtin_fmaxf(
+          __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(rlo.x), __builtin_fabsf(rlo.y)), __builtin_fabsf(rlo.z)),
+          __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(rhi.x), __builtin_fabsf(rhi.y)), __builtin_fabsf(rhi.z)));
+      const float need = 0x1p-20f * (rmax + 2.0f * (__builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.o.x),
+                                                                                   __builtin_fabsf(r.o.y)),
+                                                                    __builtin_fabsf(r.o.z)) + best * dmax));
+      if (__builtin_fminf(__builtin_fminf(mx, my), mz) > __builtin_fminf(bound, need)) return true;
+
     }
   }
   const float2 pm = pmargin_of<F>(S)[best_prim];
