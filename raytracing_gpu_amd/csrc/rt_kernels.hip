@@ -816,7 +816,7 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
       const float my = __builtin_fminf(p.y - (c.y - rad), (c.y + rad) - p.y);
       const float mz = __builtin_fminf(p.z - (c.z - rad), (c.z + rad) - p.z);
       // the chain check's per-ancestor margin below, taken at its largest: the root box's magnitude
-      const float4 rlo = S.nodes[2 * base], rhi = S.nodes[2 * base + 1];
+      const float4 rlo = nodes_of<F>(S)[2 * base], rhi = nodes_of<F>(S)[2 * base + 1];
       const float rmax = __builtin_fmaxf(
           __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(rlo.x), __builtin_fabsf(rlo.y)), __builtin_fabsf(rlo.z)),
           __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(rhi.x), __builtin_fabsf(rhi.y)), __builtin_fabsf(rhi.z)));
