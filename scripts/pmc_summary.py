@@ -31,21 +31,34 @@ try:
                                      text=True).stdout.strip() or None
 except OSError:
     res["git_head"] = None
+# PMC_LAST=N: only the last N dispatches of the kernel in each pass (bench.py's timed steps; its
+# earlier launches -- module load, cold draws, the measuring launch -- are other shapes or schedules)
+last = int(os.environ.get("PMC_LAST", "0"))
+res["dispatch_selection"] = f"last {last} dispatches of each pass (the timed steps)" if last else "all dispatches"
 for p in (f"{name}_fetch", f"{name}_write", f"{name}_sq", f"{name}_sq2", f"{name}_sq3", f"{name}_l2"):
     per = defaultdict(lambda: defaultdict(float))
     for f in glob.glob(f"gpurun_out/{p}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             if kname not in row.get("Kernel_Name", ""):
                 continue
-            per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
+            per[row["Counter_Name"]][int(row["Dispatch_Id"])] += float(row["Counter_Value"])
     for c, d in per.items():
-        res[c] = sum(d.values()) / len(d)
-        res["dispatches"][p] = len(d)
+        keys = sorted(d)[-last:] if last else sorted(d)
+        res[c] = sum(d[k] for k in keys) / len(keys)
+        res["dispatches"][p] = len(keys)
 for f in glob.glob(f"gpurun_out/{name}_trace/**/*kernel_stats.csv", recursive=True):
     for row in csv.DictReader(open(f)):
         if kname in row["Name"]:
             res.setdefault("trace", []).append({"name": row["Name"][:120], "calls": int(row["Calls"]),
                                                 "avg_ms": float(row["AverageNs"]) / 1e6})
+if last:  # the same dispatches' durations from the kernel trace
+    for f in glob.glob(f"gpurun_out/{name}_trace/**/*kernel_trace.csv", recursive=True):
+        rows = [r for r in csv.DictReader(open(f)) if kname in r["Kernel_Name"]]
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows[-last:]]
+        if durs:
+            res["timed_dispatch_ms"] = [round(x, 4) for x in durs]
+            res["timed_avg_ms"] = sum(durs) / len(durs)
 names = {t["name"] for t in res.get("trace", [])}
 if len(names) == 1:  # the full instantiation, e.g. render_step_kernel<25730>: bench.py matches on it
     n = names.pop()
