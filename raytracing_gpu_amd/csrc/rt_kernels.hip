@@ -2573,13 +2573,16 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
     // lanes of the stepwise kernel that runs the split launches (4 waves/SIMD: 1024 per CU),
     // whatever variant measured (bench.py measures with the counting variant)
     const double lanes = (double)c->cus * 1024.0;
-    // Long items (spp > 16, e.g. C2's primary 1 x 100 split) are split only above a third of a
-    // lane's share: splitting them all turns the launch into one refill per sample (C2 1 x 100,
-    // N = 1 warm: every item split 24.9 ms; above 300 segments 19.4, 400: 20.9, 600: 25.4 ms; the
-    // N = 8 share (117 segments per lane) needs <= 100: 3.2 ms, 300: 8.2 ms).
+    // Long items (spp > 16, e.g. C2's primary 1 x 100 split): splitting them all turns the launch
+    // into one refill per sample, so a full frame splits only above a third of a lane's share and a
+    // small share above 100 segments (C2 1 x 100 warm, by threshold: N = 1 (925 segments per lane)
+    // every item 24.9 ms, 300: 19.4, 400: 20.9, 600: 25.4; N = 2 (462) 50: 12.3, 100: 11.4, 200:
+    // 13.6, 400: 15.2; N = 4 (231) 100: 6.0, 300: 10.1; N = 8 (117) 53: 3.2, 100: 3.4, 300: 8.2 ms).
     const double share = (double)segs / lanes;
     double thr = (double)items >= 6.0 * lanes ? std::max(32.0, 0.5 * share)
-                                               : (spp <= 16 ? 24.0 : std::max(24.0, 0.33 * share));
+                                               : (spp <= 16 ? 24.0
+                                                             : (share >= 800.0 ? 0.33 * share
+                                                                               : std::max(24.0, std::min(100.0, 0.45 * share))));
     if (const char* e = getenv("RT_SPLIT_MIN_SEGMENTS")) thr = atof(e);  // tuning
     const long long bt = (long long)std::ceil(thr / (double)(1 << shift));
     long long ns = 0;

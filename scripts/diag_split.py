@@ -17,7 +17,7 @@ W, H = 1200, 800
 ctx = rt.Context(0)
 ctx.render_init(W, H, 1984)
 sc = rt.Scene.builtin("big1")
-for n in (1, 8):
+for n in [int(x) for x in os.environ.get("DIAG_N", "1,8").split(",")]:
     args = rt.make_args(W, H, spp, 0, nfb, 50, 0, band_rows=4, band_first=0, band_stride=n)
     fb = torch.empty(nfb * len(rt.owned_rows(args)) * W * 3, dtype=torch.float32, device="cuda")
     res = []
