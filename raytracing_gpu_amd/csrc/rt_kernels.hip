@@ -1448,9 +1448,13 @@ constexpr int render_wpe() {
 #ifndef RT_WPE_FINAL
 #define RT_WPE_FINAL 4
 #endif
+#ifndef RT_WPE_MESH
+#define RT_WPE_MESH 4
+#endif
   return (F & F_LDS) != 0 ? 1
                           : (feat == F_FINAL ? RT_WPE_FINAL
-                                             : ((feat == F_CORNELL || feat == F_MESH) ? 4 : (feat == F_ALL ? 3 : 1)));
+                                             : (feat == F_MESH ? RT_WPE_MESH
+                                                               : (feat == F_CORNELL ? 4 : (feat == F_ALL ? 3 : 1))));
 #endif
 }
 template <int F>
