@@ -1335,13 +1335,18 @@ struct RenderParams {
   // state at every sample start into ckpt[pos * spp + s]; split_mode 2: their samples are separate
   // work items (claim k < n_split * spp: position k / spp, sample k % spp) that start from ckpt
   // (sample 0: from states) and write the sample's sum to contrib[3 k]; merge_split_kernel adds
-  // them up in sample order.  cam_st[s]: the REF camera state at sample s's start.
+  // them up in sample order.  cam_st[s]: the REF camera state at sample s's start.  order (split_mode
+  // 2, may be null): claim k takes order[k] instead of k -- split samples and the other items in
+  // one longest-first sequence by the recording launch's per-sample segment counts (split_mode 1
+  // keeps them in ckpt's spare word: segments before sample s at [pos * spp + s], the item's
+  // total at [pos * spp]).
   int split_mode;
   int pad5;
   unsigned long long n_split;
   uint4* ckpt;
   float* contrib;
   const uint4* cam_st;
+  const uint32_t* order;
   // Camera-ray candidate lists (render_step_kernel; null: camera rays traverse the tree): per 8x8
   // tile of the image, tile_cnt[t] (id, nearest) pairs at tile_ent[2 * t * tile_cap] (-1: the tile
   // overflowed).
@@ -1760,6 +1765,7 @@ void render_step_kernel(const RenderParams P) {
             }
             if (P.row_cost && (i & 15) == 0) atomicAdd(&P.row_cost[j], (unsigned long long)item_segs);
             if (P.item_cost) P.item_cost[item] = (uint16_t)(item_segs < 65535u ? item_segs : 65535u);
+            if (P.split_mode == 1 && ck >= 0) P.ckpt[2 * (long long)ck * P.spp + 1] = make_uint4(0u, 0u, item_segs, 0u);
             item = -1;
           }
         }
@@ -1783,12 +1789,13 @@ void render_step_kernel(const RenderParams P) {
             ck = -1;
             if (P.split_mode == 2) {  // split samples first, then the rest of perm
               const unsigned long long nsub = P.n_split * (unsigned long long)P.spp;
-              if (mine < nsub) {
-                pos = mine / (unsigned)P.spp;
-                sa = (int)(mine - pos * (unsigned)P.spp);
-                ck = (int)mine;
+              const unsigned long long v = P.order ? (unsigned long long)P.order[mine] : mine;
+              if (v < nsub) {
+                pos = v / (unsigned)P.spp;
+                sa = (int)(v - pos * (unsigned)P.spp);
+                ck = (int)v;
               } else {
-                pos = mine - nsub + P.n_split;
+                pos = v - nsub + P.n_split;
               }
             } else if (P.split_mode == 1 && mine < P.n_split) {
               ck = (int)mine;
@@ -1805,7 +1812,7 @@ void render_step_kernel(const RenderParams P) {
             const long long id = P.fb_first + f;
             const long long p = (long long)j * P.W + i;
             const long long slot = ((id + 1) * p + id + 1) % P.npix;  // render.h:101 (H3)
-            const uint4* st = sa > 0 ? P.ckpt + 2 * (long long)mine : P.states + 2 * slot;
+            const uint4* st = sa > 0 ? P.ckpt + 2 * (long long)ck : P.states + 2 * slot;
             const uint4 s0 = st[0], s1 = st[1];
             loc.d = s0.x; loc.v[0] = s0.y; loc.v[1] = s0.z; loc.v[2] = s0.w; loc.v[3] = s1.x; loc.v[4] = s1.y;
             s = sa;
@@ -1855,7 +1862,7 @@ void render_step_kernel(const RenderParams P) {
           if (P.split_mode == 1 && ck >= 0 && s > 0) {  // record the sample-start state for split launches
             uint4* dst = P.ckpt + 2 * ((long long)ck * P.spp + s);
             dst[0] = make_uint4(loc.d, loc.v[0], loc.v[1], loc.v[2]);
-            dst[1] = make_uint4(loc.v[3], loc.v[4], 0u, 0u);
+            dst[1] = make_uint4(loc.v[3], loc.v[4], item_segs, 0u);
           }
           const float u = ((float)i + rtx::uniform(loc)) / (float)P.W;
           const float v = ((float)j + rtx::uniform(loc)) / (float)P.H;
@@ -2038,6 +2045,21 @@ __global__ __launch_bounds__(kBlock) void merge_split_kernel(const RenderParams 
   dst[2] = out.z;
 }
 
+// Segment count of every split sample k = pos * spp + s of the recording launch (split_mode 1):
+// the difference of the item's segment counts at consecutive sample starts (ckpt's spare word),
+// the last sample's up to the item's total (kept at sample 0's record).  Clamped to 255.
+__global__ __launch_bounds__(kBlock) void split_len_kernel(const uint4* __restrict__ ckpt, unsigned long long nsub,
+                                                           int spp, uint8_t* __restrict__ len) {
+  const unsigned long long k = (unsigned long long)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= nsub) return;
+  const unsigned long long pos = k / (unsigned)spp;
+  const int s = (int)(k - pos * (unsigned)spp);
+  const unsigned st = s > 0 ? ckpt[2 * k + 1].z : 0u;
+  const unsigned en = s + 1 < spp ? ckpt[2 * (k + 1) + 1].z : ckpt[2 * pos * spp + 1].z;
+  const unsigned d = en >= st ? en - st : 0u;
+  len[k] = (uint8_t)(d < 255u ? d : 255u);
+}
+
 // Camera-ray culling per 8x8-pixel tile.  A camera ray (render.h:105-108, camera.h:49-58) is
 //   X(t) = O + off + t (F - O - off),  F = lower_left + u horizontal + v vertical,
 // with (u, v) inside the tile (jitter in [0, 1] of a pixel), |off| <= lens_radius = L and its time
@@ -2200,6 +2222,13 @@ struct rt_ctx {
   long long contrib_cap = 0;  // floats
   uint4* cam_st = nullptr;
   long long cam_st_cap = 0;  // uint4 pairs
+  // Claim order of the split launches (RenderParams::order), built on the first one after a
+  // recording; rest_key: cost bucket of each unsplit perm position (from n_split on).
+  uint32_t* order = nullptr;
+  long long order_cap = 0;
+  bool order_ok = false;
+  std::vector<uint16_t> rest_key;
+  int rest_shift = 0;
   long long cam_st_key[3] = {-1, -1, -1};
   long long scene_gen = 0;
   int cus = 0, blocks_per_cu[32] = {0};  // per kernel variant (kVariants)
@@ -2566,27 +2595,25 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
   HIPCHK(c, hipMemcpyAsync(c->perm, pm.data(), pm.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->n_long = (unsigned long long)nl;
-  // Items that can decide when a launch ends have their samples split on later launches: in a
-  // small share (< 6 items per resident lane, as for the camera lists) every item of >= 24
-  // segments, else items longer than half a resident lane's share of the segments (at least 32).
-  // They are the first positions of perm (cost buckets descending).  C2, one GPU per rank's
-  // share: N = 8 share 3.59 -> 2.88 ms with 24 (3.34 ms with the large-share rule, 3.15 with
-  // 12); at N = 1 and 2 a fixed 24 costs 3.5 % and 2 % (the split samples' extra claims and
-  // state loads), hence the rule by share size.
+  // Items that can decide when a launch ends have their samples split on later launches: the
+  // items at or above a threshold set by the share's size (below).  They are the first positions
+  // of perm (cost buckets descending).  (Round 2, samples still claimed in item order: C2's N = 8
+  // share 3.59 -> 2.88 ms.)
   {
     // lanes of the stepwise kernel that runs the split launches (4 waves/SIMD: 1024 per CU),
     // whatever variant measured (bench.py measures with the counting variant)
     const double lanes = (double)c->cus * 1024.0;
-    // Long items (spp > 16, e.g. C2's primary 1 x 100 split): splitting them all turns the launch
-    // into one refill per sample, so a full frame splits only above a third of a lane's share and a
-    // small share above 100 segments (C2 1 x 100 warm, by threshold: N = 1 (925 segments per lane)
-    // every item 24.9 ms, 300: 19.4, 400: 20.9, 600: 25.4; N = 2 (462) 50: 12.3, 100: 11.4, 200:
-    // 13.6, 400: 15.2; N = 4 (231) 100: 6.0, 300: 10.1; N = 8 (117) 53: 3.2, 100: 3.4, 300: 8.2 ms).
-    const double share = (double)segs / lanes;
-    double thr = (double)items >= 6.0 * lanes ? std::max(32.0, 0.5 * share)
-                                               : (spp <= 16 ? 24.0
-                                                             : (share >= 800.0 ? 0.33 * share
-                                                                               : std::max(24.0, std::min(100.0, 0.45 * share))));
+    // Split launches claim everything longest first (RenderParams::order), so an unsplit item
+    // only needs to be short against a lane's share; every split costs claims and state loads, and
+    // a sky pixel (one segment per sample) gains nothing from it.  Measured, C2 warm by threshold
+    // (camera lists on), 10 x 10: N = 8 (4.6 items and 117 segments per lane) 24: 2.53, 32: 2.34,
+    // 48: 2.62 ms; N = 4 (9.2, 231) 24: 4.82, 32: 4.43, 48: 4.55, 115: 4.72; N = 2 (18, 462) 32:
+    // 8.54, 48: 8.39, 231: 8.57; N = 1 (36, 925) 48: 16.56, 462: 16.53.  1 x 100: N = 8 85: 3.08,
+    // 100: 2.81, 120: 2.79; N = 4 100: 5.39, 150: 5.28, 200: 5.31, 250: 6.27; N = 2 200: 10.93,
+    // 300: 9.09, 400: 11.32; N = 1 200: 21.59, 300: 16.69, 400: 18.44.
+    const double share = (double)segs / lanes, per_lane = (double)items / lanes;
+    double thr = spp <= 16 ? (per_lane < 6.0 ? 32.0 : per_lane < 24.0 ? 48.0 : std::max(32.0, 0.5 * share))
+                           : std::min(3.0 * spp, std::max(1.04 * spp, 0.85 * share));
     if (const char* e = getenv("RT_SPLIT_MIN_SEGMENTS")) thr = atof(e);  // tuning
     const long long bt = (long long)std::ceil(thr / (double)(1 << shift));
     long long ns = 0;
@@ -2594,6 +2621,10 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
     if (ns * (long long)spp >= (1LL << 30)) ns = 0;
     c->n_split = (unsigned long long)ns;
     c->split_state = ns > 0 ? 0 : -1;
+    c->order_ok = false;
+    c->rest_key.resize((size_t)(items - ns));
+    for (long long k = ns; k < items; ++k) c->rest_key[(size_t)(k - ns)] = ic[(size_t)pm[(size_t)k]];
+    c->rest_shift = shift;
   }
   return RT_OK;
 }
@@ -2686,6 +2717,7 @@ int rt_ctx_destroy(rt_ctx* c) {
   if (c->tiles) (void)hipFree(c->tiles);
   if (c->cam_tab) (void)hipFree(c->cam_tab);
   if (c->ckpt) (void)hipFree(c->ckpt);
+  if (c->order) (void)hipFree(c->order);
   if (c->contrib) (void)hipFree(c->contrib);
   if (c->cam_st) (void)hipFree(c->cam_st);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -3137,6 +3169,49 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
                                hipMemcpyHostToDevice, c->stream));
       std::copy(skey, skey + 3, c->cam_st_key);
     }
+    // Split launches claim split samples and unsplit items in one sequence, longest first by the
+    // recording launch's counts (the long samples of a small share start with the launch instead of
+    // trailing it).  Built once per recording; results do not depend on the order.
+    const long long rest = items - (long long)c->n_split;
+    const char* oe = getenv("RT_SPLIT_ORDER");  // tuning: 0 = samples in item order, then the rest
+    if (split_mode == 2 && (long long)c->rest_key.size() == rest && !(oe && atoi(oe) == 0)) {
+      const long long total = need + rest;
+      if (!c->order_ok) {
+        if (total > c->order_cap) {
+          if (c->order) HIPCHK(c, hipFree(c->order));
+          c->order = nullptr;
+          c->order_cap = 0;
+          HIPCHK(c, hipMalloc((void**)&c->order, (size_t)total * sizeof(uint32_t)));
+          c->order_cap = total;
+        }
+        std::vector<uint8_t> len((size_t)need);
+        split_len_kernel<<<(unsigned)((need + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
+            c->ckpt, (unsigned long long)need, a->spp, (uint8_t*)c->order);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(len.data(), c->order, len.size(), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const int sh = c->rest_shift;
+        auto rkey = [&](long long r) {
+          return (int)std::min(65535LL, ((long long)c->rest_key[(size_t)r] << sh) + ((1LL << sh) >> 1));
+        };
+        std::vector<long long> at(65537, 0);  // counting sort, longest first; samples before items of equal key
+        for (long long k = 0; k < need; ++k) ++at[len[(size_t)k]];
+        for (long long r = 0; r < rest; ++r) ++at[rkey(r)];
+        long long acc = 0;
+        for (int v = 65535; v >= 0; --v) {
+          const long long h = at[v];
+          at[v] = acc;
+          acc += h;
+        }
+        std::vector<uint32_t> ord((size_t)total);
+        for (long long k = 0; k < need; ++k) ord[(size_t)at[len[(size_t)k]]++] = (uint32_t)k;
+        for (long long r = 0; r < rest; ++r) ord[(size_t)at[rkey(r)]++] = (uint32_t)(need + r);
+        HIPCHK(c, hipMemcpyAsync(c->order, ord.data(), ord.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->order_ok = true;
+      }
+      P.order = c->order;
+    }
     P.split_mode = split_mode;
     P.n_split = c->n_split;
     P.ckpt = c->ckpt;
@@ -3279,6 +3354,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   }
   if (split_mode == 1) {  // sample-start states recorded for this seed
     c->split_state = 1;
+    c->order_ok = false;
     c->split_seed = a->seed;
   }
   HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
