@@ -3194,18 +3194,24 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
         auto rkey = [&](long long r) {
           return (int)std::min(65535LL, ((long long)c->rest_key[(size_t)r] << sh) + ((1LL << sh) >> 1));
         };
-        std::vector<long long> at(65537, 0);  // counting sort, longest first; samples before items of equal key
+        // samples by length (counting sort, longest first), merged with the unsplit positions (already
+        // longest first in perm); samples go before items of equal key
+        long long at[256] = {0};
         for (long long k = 0; k < need; ++k) ++at[len[(size_t)k]];
-        for (long long r = 0; r < rest; ++r) ++at[rkey(r)];
         long long acc = 0;
-        for (int v = 65535; v >= 0; --v) {
+        for (int v = 255; v >= 0; --v) {
           const long long h = at[v];
           at[v] = acc;
           acc += h;
         }
+        std::vector<uint32_t> sub((size_t)need);
+        for (long long k = 0; k < need; ++k) sub[(size_t)at[len[(size_t)k]]++] = (uint32_t)k;
         std::vector<uint32_t> ord((size_t)total);
-        for (long long k = 0; k < need; ++k) ord[(size_t)at[len[(size_t)k]]++] = (uint32_t)k;
-        for (long long r = 0; r < rest; ++r) ord[(size_t)at[rkey(r)]++] = (uint32_t)(need + r);
+        long long o = 0, si = 0, ri = 0;
+        while (si < need || ri < rest) {
+          if (ri < rest && (si == need || rkey(ri) > (int)len[sub[(size_t)si]])) ord[(size_t)o++] = (uint32_t)(need + ri++);
+          else ord[(size_t)o++] = sub[(size_t)si++];
+        }
         HIPCHK(c, hipMemcpyAsync(c->order, ord.data(), ord.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         c->order_ok = true;
