@@ -2060,6 +2060,101 @@ __global__ __launch_bounds__(kBlock) void split_len_kernel(const uint4* __restri
   len[k] = (uint8_t)(d < 255u ? d : 255u);
 }
 
+// Claim order of a split launch, built on the device from the sample lengths (split_len_kernel)
+// and the unsplit positions' cost groups (host tables; `kOrderKeys` keys: a sample's length, an
+// unsplit position's bucket midpoint clamped to 256 -- every sample key is < 256):
+//   sample k of key v   -> sub_base[v] + its rank among the samples of key v, in k order (a
+//                          stable counting sort: neighbouring samples keep their order, as the
+//                          coherence of the claims needs -- an atomic-order scatter measured
+//                          1.5-4 % slower launches)
+//   unsplit position r  -> r + (samples with key >= key(r)), key(r) from rest_gt (unsplit
+//                          positions with key > v, non-increasing in v; perm is longest first)
+// so samples precede unsplit positions of an equal key.  Results do not depend on the order.
+// The sort runs over tiles of kOrderTile samples, one wave per tile: per-tile histograms, a scan
+// per key over the tiles, then each tile's samples ranked in order with ballots.
+constexpr int kOrderKeys = 257;
+constexpr int kOrderTile = 4096;
+__global__ __launch_bounds__(64) void order_tile_hist_kernel(const uint8_t* __restrict__ len, unsigned long long n,
+                                                             unsigned* __restrict__ tile_hist) {
+  __shared__ unsigned h[256];
+  for (int v = threadIdx.x; v < 256; v += 64) h[v] = 0;
+  __syncthreads();
+  const unsigned long long k0 = (unsigned long long)blockIdx.x * kOrderTile;
+  for (int q = threadIdx.x; q < kOrderTile; q += 64)
+    if (k0 + q < n) atomicAdd(&h[len[k0 + q]], 1u);
+  __syncthreads();
+  for (int v = threadIdx.x; v < 256; v += 64) tile_hist[(size_t)blockIdx.x * 256 + v] = h[v];
+}
+// One block per key: exclusive prefix over the tiles (in place), the key's total into total[v].
+__global__ __launch_bounds__(256) void order_scan_kernel(unsigned* __restrict__ tile_hist, unsigned tiles,
+                                                         unsigned* __restrict__ total) {
+  __shared__ unsigned part[256];
+  const unsigned v = blockIdx.x, per = (tiles + 255) / 256, t0 = threadIdx.x * per;
+  unsigned sum = 0;
+  for (unsigned t = t0; t < t0 + per && t < tiles; ++t) sum += tile_hist[(size_t)t * 256 + v];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned acc = 0;
+    for (int q = 0; q < 256; ++q) {
+      const unsigned x = part[q];
+      part[q] = acc;
+      acc += x;
+    }
+    total[v] = acc;
+  }
+  __syncthreads();
+  unsigned acc = part[threadIdx.x];
+  for (unsigned t = t0; t < t0 + per && t < tiles; ++t) {
+    const unsigned x = tile_hist[(size_t)t * 256 + v];
+    tile_hist[(size_t)t * 256 + v] = acc;
+    acc += x;
+  }
+}
+// tab: sub_base[256], sub_ge[kOrderKeys], rest_gt[kOrderKeys]
+__global__ __launch_bounds__(64) void order_scatter_kernel(const uint8_t* __restrict__ len, unsigned long long need,
+                                                           const unsigned* __restrict__ tile_off,
+                                                           const unsigned* __restrict__ tab, uint32_t* __restrict__ order) {
+  __shared__ unsigned cnt[256];
+  for (int v = threadIdx.x; v < 256; v += 64) cnt[v] = tab[v] + tile_off[(size_t)blockIdx.x * 256 + v];
+  __syncthreads();
+  const unsigned long long k0 = (unsigned long long)blockIdx.x * kOrderTile;
+  const unsigned lane = threadIdx.x;
+  for (int q = 0; q < kOrderTile; q += 64) {
+    const unsigned long long k = k0 + q + lane;
+    if (k0 + q >= need) break;  // wave-uniform
+    bool pending = k < need;
+    const unsigned v = pending ? len[k] : 0u;
+    while (__ballot(pending) != 0) {  // one pass per distinct key among the 64
+      const unsigned long long act = __ballot(pending);
+      const unsigned lead = __shfl(v, __ffsll((long long)act) - 1, 64);
+      const unsigned long long m = __ballot(pending && v == lead);
+      const unsigned base = cnt[lead];
+      if (pending && v == lead) {
+        order[base + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)k;
+        pending = false;
+      }
+      __syncthreads();  // every lane has read cnt[lead] (one wave: a barrier of the wave)
+      if (lane == 0) cnt[lead] = base + (unsigned)__popcll(m);
+      __syncthreads();
+    }
+  }
+}
+__global__ __launch_bounds__(kBlock) void order_rest_kernel(unsigned long long need, unsigned long long rest,
+                                                            const unsigned* __restrict__ tab, uint32_t* __restrict__ order) {
+  const unsigned long long r = (unsigned long long)blockIdx.x * kBlock + threadIdx.x;
+  if (r >= rest) return;
+  const unsigned* sub_ge = tab + 256;
+  const unsigned* rest_gt = tab + 256 + kOrderKeys;
+  int lo = 0, hi = kOrderKeys - 1;  // smallest key v with rest_gt[v] <= r (= r's key)
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (rest_gt[mid] <= (unsigned)r) hi = mid;
+    else lo = mid + 1;
+  }
+  order[r + sub_ge[lo]] = (uint32_t)(need + r);
+}
+
 // Camera-ray culling per 8x8-pixel tile.  A camera ray (render.h:105-108, camera.h:49-58) is
 //   X(t) = O + off + t (F - O - off),  F = lower_left + u horizontal + v vertical,
 // with (u, v) inside the tile (jitter in [0, 1] of a pixel), |off| <= lens_radius = L and its time
@@ -2223,12 +2318,16 @@ struct rt_ctx {
   uint4* cam_st = nullptr;
   long long cam_st_cap = 0;  // uint4 pairs
   // Claim order of the split launches (RenderParams::order), built on the first one after a
-  // recording; rest_key: cost bucket of each unsplit perm position (from n_split on).
+  // recording (order_scatter_kernel); rest_gt[v]: unsplit perm positions (from n_split on) whose
+  // key -- cost bucket midpoint, clamped to 256 -- exceeds v; order_tab: the kernel's tables, its
+  // histogram and cursors (order_tab_host: the host copy of the tables).
   uint32_t* order = nullptr;
   long long order_cap = 0;
   bool order_ok = false;
-  std::vector<uint16_t> rest_key;
-  int rest_shift = 0;
+  long long rest_n = -1;
+  std::vector<unsigned> rest_gt;
+  unsigned* order_tab = nullptr;
+  std::vector<unsigned> order_tab_host;
   long long cam_st_key[3] = {-1, -1, -1};
   long long scene_gen = 0;
   int cus = 0, blocks_per_cu[32] = {0};  // per kernel variant (kVariants)
@@ -2622,9 +2721,12 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
     c->n_split = (unsigned long long)ns;
     c->split_state = ns > 0 ? 0 : -1;
     c->order_ok = false;
-    c->rest_key.resize((size_t)(items - ns));
-    for (long long k = ns; k < items; ++k) c->rest_key[(size_t)(k - ns)] = ic[(size_t)pm[(size_t)k]];
-    c->rest_shift = shift;
+    c->rest_n = items - ns;
+    c->rest_gt.assign(kOrderKeys, 0u);
+    for (long long b = 0; b < bt && b < 65536; ++b) {  // the unsplit buckets
+      const long long key = std::min(256LL, (b << shift) + ((1LL << shift) >> 1));
+      for (long long v = 0; v < key; ++v) c->rest_gt[(size_t)v] += (unsigned)hist[(size_t)b];
+    }
   }
   return RT_OK;
 }
@@ -2718,6 +2820,7 @@ int rt_ctx_destroy(rt_ctx* c) {
   if (c->cam_tab) (void)hipFree(c->cam_tab);
   if (c->ckpt) (void)hipFree(c->ckpt);
   if (c->order) (void)hipFree(c->order);
+  if (c->order_tab) (void)hipFree(c->order_tab);
   if (c->contrib) (void)hipFree(c->contrib);
   if (c->cam_st) (void)hipFree(c->cam_st);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -3174,7 +3277,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     // trailing it).  Built once per recording; results do not depend on the order.
     const long long rest = items - (long long)c->n_split;
     const char* oe = getenv("RT_SPLIT_ORDER");  // tuning: 0 = samples in item order, then the rest
-    if (split_mode == 2 && (long long)c->rest_key.size() == rest && !(oe && atoi(oe) == 0)) {
+    if (split_mode == 2 && c->rest_n == rest && !(oe && atoi(oe) == 0)) {
       const long long total = need + rest;
       if (!c->order_ok) {
         if (total > c->order_cap) {
@@ -3184,36 +3287,47 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
           HIPCHK(c, hipMalloc((void**)&c->order, (size_t)total * sizeof(uint32_t)));
           c->order_cap = total;
         }
-        std::vector<uint8_t> len((size_t)need);
+        constexpr int kTab = 256 + 2 * kOrderKeys;  // then the key totals (256)
+        if (!c->order_tab) HIPCHK(c, hipMalloc((void**)&c->order_tab, (size_t)(kTab + 256) * sizeof(unsigned)));
+        // scratch in contrib (12 B per sample; this launch writes it only later): the lengths
+        // (1 B per sample), then the per-tile histograms / offsets (1 KB per 4096 samples)
+        const unsigned tiles = (unsigned)((need + kOrderTile - 1) / kOrderTile);
+        const long long scratch = ((need + 255) & ~255LL) + (long long)tiles * 256 * 4;
+        if (scratch > 4 * c->contrib_cap) {  // tiny splits: 12 B per sample is less than one tile's table
+          if (c->contrib) HIPCHK(c, hipFree(c->contrib));
+          c->contrib = nullptr;
+          c->contrib_cap = 0;
+          HIPCHK(c, hipMalloc((void**)&c->contrib, (size_t)scratch));
+          c->contrib_cap = scratch / 4;
+        }
+        uint8_t* len = (uint8_t*)c->contrib;
+        unsigned* tile_hist = (unsigned*)(len + ((need + 255) & ~255LL));
         split_len_kernel<<<(unsigned)((need + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
-            c->ckpt, (unsigned long long)need, a->spp, (uint8_t*)c->order);
+            c->ckpt, (unsigned long long)need, a->spp, len);
         HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipMemcpyAsync(len.data(), c->order, len.size(), hipMemcpyDeviceToHost, c->stream));
+        order_tile_hist_kernel<<<tiles, 64, 0, c->stream>>>(len, (unsigned long long)need, tile_hist);
+        HIPCHK(c, hipGetLastError());
+        order_scan_kernel<<<256, 256, 0, c->stream>>>(tile_hist, tiles, c->order_tab + kTab);
+        HIPCHK(c, hipGetLastError());
+        unsigned hist[256];
+        HIPCHK(c, hipMemcpyAsync(hist, c->order_tab + kTab, sizeof(hist), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        const int sh = c->rest_shift;
-        auto rkey = [&](long long r) {
-          return (int)std::min(65535LL, ((long long)c->rest_key[(size_t)r] << sh) + ((1LL << sh) >> 1));
-        };
-        // samples by length (counting sort, longest first), merged with the unsplit positions (already
-        // longest first in perm); samples go before items of equal key
-        long long at[256] = {0};
-        for (long long k = 0; k < need; ++k) ++at[len[(size_t)k]];
-        long long acc = 0;
-        for (int v = 255; v >= 0; --v) {
-          const long long h = at[v];
-          at[v] = acc;
-          acc += h;
+        std::vector<unsigned>& t = c->order_tab_host;
+        t.assign(kTab, 0u);
+        unsigned* sub_base = t.data();
+        unsigned* sub_ge = t.data() + 256;
+        unsigned* rest_gt = t.data() + 256 + kOrderKeys;
+        for (int v = 255; v >= 0; --v) sub_ge[v] = sub_ge[v + 1] + hist[v];  // sub_ge[256] = 0
+        for (int v = 0; v < 256; ++v) sub_base[v] = c->rest_gt[(size_t)v] + sub_ge[v + 1];
+        std::copy(c->rest_gt.begin(), c->rest_gt.end(), rest_gt);
+        HIPCHK(c, hipMemcpyAsync(c->order_tab, t.data(), t.size() * sizeof(unsigned), hipMemcpyHostToDevice, c->stream));
+        order_scatter_kernel<<<tiles, 64, 0, c->stream>>>(len, (unsigned long long)need, tile_hist, c->order_tab, c->order);
+        HIPCHK(c, hipGetLastError());
+        if (rest > 0) {
+          order_rest_kernel<<<(unsigned)((rest + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
+              (unsigned long long)need, (unsigned long long)rest, c->order_tab, c->order);
+          HIPCHK(c, hipGetLastError());
         }
-        std::vector<uint32_t> sub((size_t)need);
-        for (long long k = 0; k < need; ++k) sub[(size_t)at[len[(size_t)k]]++] = (uint32_t)k;
-        std::vector<uint32_t> ord((size_t)total);
-        long long o = 0, si = 0, ri = 0;
-        while (si < need || ri < rest) {
-          if (ri < rest && (si == need || rkey(ri) > (int)len[sub[(size_t)si]])) ord[(size_t)o++] = (uint32_t)(need + ri++);
-          else ord[(size_t)o++] = sub[(size_t)si++];
-        }
-        HIPCHK(c, hipMemcpyAsync(c->order, ord.data(), ord.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
         c->order_ok = true;
       }
       P.order = c->order;

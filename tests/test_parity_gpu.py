@@ -486,16 +486,21 @@ def test_camera_lists_on_and_off(rtlib, gpu_ctx, oracle, threshold, monkeypatch)
     assert cnt["segments"] == segs
 
 
+@pytest.mark.parametrize("order", [None, "0"], ids=["longest_first", "item_order"])
 @pytest.mark.parametrize("min_segs", [None, "1"], ids=["default", "every_item"])
 @pytest.mark.parametrize("band", [None, (4, 1, 3)], ids=["full", "share"])
-def test_split_samples_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch, min_segs, band):
+def test_split_samples_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch, min_segs, band, order):
     """Warm launches split the samples of the longest items over work items (launch 1 measures,
-    launch 2 records the sample-start RNG states, launches 3+ split and merge): every launch's
-    frame buffer equals the oracle's bit for bit, with the same segment and sample counts."""
+    launch 2 records the sample-start RNG states and segment counts, launches 3+ claim the split
+    samples and the other items longest first -- or, RT_SPLIT_ORDER=0, samples in item order -- and
+    merge): every launch's frame buffer equals the oracle's bit for bit, with the same segment and
+    sample counts."""
     import torch
 
     if min_segs:
         monkeypatch.setenv("RT_SPLIT_MIN_SEGMENTS", min_segs)
+    if order is not None:
+        monkeypatch.setenv("RT_SPLIT_ORDER", order)
     W, H, spp, nfb = 96, 54, 4, 2
     sc = rtlib.Scene.builtin("big1")
     gpu_ctx.upload(sc)  # new scene generation: a fresh schedule
