@@ -2140,6 +2140,13 @@ __global__ __launch_bounds__(64) void order_scatter_kernel(const uint8_t* __rest
     }
   }
 }
+// Sort keys of the item schedule: the measuring launch's segment count in buckets of 2^shift,
+// clamped to the top bucket 255 (items of >= 255 * 2^shift segments keep their natural order).
+__global__ __launch_bounds__(kBlock) void cost_key_kernel(const uint16_t* __restrict__ cost, unsigned long long n,
+                                                          int shift, uint8_t* __restrict__ key) {
+  const unsigned long long k = (unsigned long long)blockIdx.x * kBlock + threadIdx.x;
+  if (k < n) key[k] = (uint8_t)min(255u, (unsigned)cost[k] >> shift);
+}
 __global__ __launch_bounds__(kBlock) void order_rest_kernel(unsigned long long need, unsigned long long rest,
                                                             const unsigned* __restrict__ tab, uint32_t* __restrict__ order) {
   const unsigned long long r = (unsigned long long)blockIdx.x * kBlock + threadIdx.x;
@@ -2328,6 +2335,9 @@ struct rt_ctx {
   std::vector<unsigned> rest_gt;
   unsigned* order_tab = nullptr;
   std::vector<unsigned> order_tab_host;
+  // scratch of the device sorts (sort_keys / sort_scatter): keys, then per-tile tables
+  uint8_t* sort_scratch = nullptr;
+  long long sort_scratch_cap = 0;
   long long cam_st_key[3] = {-1, -1, -1};
   long long scene_gen = 0;
   int cus = 0, blocks_per_cu[32] = {0};  // per kernel variant (kVariants)
@@ -2656,43 +2666,89 @@ void camera_table(const rt_camera& C, uint64_t seed, int spp, std::vector<float4
   }
 }
 
+// Stable descending counting sort of n one-byte keys on the context's stream (order_*_kernel):
+// sort_keys returns the scratch key array to fill; sort_hist leaves the per-tile offsets in scratch
+// and returns the 256 key totals on the host; sort_scatter writes out[base[v] + rank] = k for every
+// key v (base: device array of 256, the caller's layout).
+constexpr int kOrderTabWords = 256 + 2 * kOrderKeys + 256;  // base, sub_ge, rest_gt, key totals
+uint8_t* sort_keys(rt_ctx* c, long long n) {
+  const long long tiles = (n + kOrderTile - 1) / kOrderTile;
+  const long long need = ((n + 255) & ~255LL) + tiles * 256 * 4;
+  if (need > c->sort_scratch_cap) {
+    if (c->sort_scratch) (void)hipFree(c->sort_scratch);
+    c->sort_scratch = nullptr;
+    c->sort_scratch_cap = 0;
+    if (hipMalloc((void**)&c->sort_scratch, (size_t)need) != hipSuccess) return nullptr;
+    c->sort_scratch_cap = need;
+  }
+  if (!c->order_tab && hipMalloc((void**)&c->order_tab, kOrderTabWords * sizeof(unsigned)) != hipSuccess) return nullptr;
+  return c->sort_scratch;
+}
+int sort_hist(rt_ctx* c, long long n, unsigned hist[256]) {
+  const unsigned tiles = (unsigned)((n + kOrderTile - 1) / kOrderTile);
+  unsigned* tile_tab = (unsigned*)(c->sort_scratch + ((n + 255) & ~255LL));
+  unsigned* totals = c->order_tab + 256 + 2 * kOrderKeys;
+  order_tile_hist_kernel<<<tiles, 64, 0, c->stream>>>(c->sort_scratch, (unsigned long long)n, tile_tab);
+  HIPCHK(c, hipGetLastError());
+  order_scan_kernel<<<256, 256, 0, c->stream>>>(tile_tab, tiles, totals);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(hist, totals, 256 * sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return RT_OK;
+}
+int sort_scatter(rt_ctx* c, long long n, const unsigned* base, uint32_t* out) {
+  const unsigned tiles = (unsigned)((n + kOrderTile - 1) / kOrderTile);
+  const unsigned* tile_tab = (const unsigned*)(c->sort_scratch + ((n + 255) & ~255LL));
+  order_scatter_kernel<<<tiles, 64, 0, c->stream>>>(c->sort_scratch, (unsigned long long)n, tile_tab, base, out);
+  HIPCHK(c, hipGetLastError());
+  return RT_OK;
+}
+
 // Item schedule of a configuration from its measuring launch's per-item segment counts (c->item_cost,
 // `segs` segments in all): perm, the long prefix and the split items.  Built when the configuration
 // is rendered again, so a single draw() does not pay the host sort.
 int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs) {
-  std::vector<uint16_t> ic((size_t)items);
-  HIPCHK(c, hipMemcpyAsync(ic.data(), c->item_cost, ic.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
   if (const char* e = getenv("RT_ITEM_COST_OUT")) {  // diagnostic: per-item segment counts
+    std::vector<uint16_t> ic((size_t)items);
+    HIPCHK(c, hipMemcpyAsync(ic.data(), c->item_cost, ic.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     if (FILE* fo = fopen(e, "wb")) {
       fwrite(ic.data(), sizeof(uint16_t), ic.size(), fo);
       fclose(fo);
     }
   }
   // Every item in descending cost buckets of 8 segments, the natural (spatially coherent) order
-  // inside a bucket; the top ~2 % by cost are the "long" prefix whose waves run at raised
+  // inside a bucket (a stable counting sort on the device; the top bucket 255 holds every item of
+  // >= 2040 segments); the top ~2 % by cost are the "long" prefix whose waves run at raised
   // priority.  (C2, one GPU as rank 0 of N: N = 8 share 3.89 -> 3.45 ms, N = 1 unchanged.)
   int shift = 3;
   if (const char* e = getenv("RT_COST_SHIFT")) shift = std::max(0, std::min(12, atoi(e)));  // tuning
-  for (uint16_t& v : ic) v = (uint16_t)(v >> shift);
-  std::vector<long long> hist(65536, 0);
-  for (uint16_t v : ic) ++hist[v];
-  std::vector<long long> start(65536, 0);  // counting sort, highest bucket first
-  long long acc = 0;
-  for (int v = 65535; v >= 0; --v) {
-    start[v] = acc;
-    acc += hist[v];
+  uint8_t* keys = sort_keys(c, items);
+  if (!keys) return fail(c, RT_ERR_HIP, "out of device memory (schedule sort)");
+  cost_key_kernel<<<(unsigned)((items + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
+      c->item_cost, (unsigned long long)items, shift, keys);
+  HIPCHK(c, hipGetLastError());
+  unsigned h[256];
+  if (int rc = sort_hist(c, items, h)) return rc;
+  std::vector<long long> hist(256);
+  for (int v = 0; v < 256; ++v) hist[(size_t)v] = h[v];
+  unsigned base[256];
+  {
+    unsigned acc = 0;
+    for (int v = 255; v >= 0; --v) {
+      base[v] = acc;
+      acc += h[v];
+    }
   }
+  HIPCHK(c, hipMemcpyAsync(c->order_tab, base, sizeof(base), hipMemcpyHostToDevice, c->stream));
+  if (int rc = sort_scatter(c, items, c->order_tab, c->perm)) return rc;
+  // completed before returning (base is on this stack): the next launch (same stream) reads perm
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   double pct = 2.0;
   if (const char* e = getenv("RT_LONG_PCT")) pct = atof(e);  // tuning
   const long long want = (long long)((double)items * pct / 100.0);
   long long nl = 0;  // whole buckets from the top while they fit in `want`
-  for (int v = 65535; v >= 0 && nl + hist[v] <= want; --v) nl += hist[v];
-  std::vector<uint32_t> pm((size_t)items);
-  for (long long k = 0; k < items; ++k) pm[(size_t)start[ic[(size_t)k]]++] = (uint32_t)k;
-  // on the context's stream, completed before returning: the next launch (same stream) reads it
-  HIPCHK(c, hipMemcpyAsync(c->perm, pm.data(), pm.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int v = 255; v >= 0 && nl + hist[(size_t)v] <= want; --v) nl += hist[(size_t)v];
   c->n_long = (unsigned long long)nl;
   // Items that can decide when a launch ends have their samples split on later launches: the
   // items at or above a threshold set by the share's size (below).  They are the first positions
@@ -2716,14 +2772,14 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
     if (const char* e = getenv("RT_SPLIT_MIN_SEGMENTS")) thr = atof(e);  // tuning
     const long long bt = (long long)std::ceil(thr / (double)(1 << shift));
     long long ns = 0;
-    for (long long v = 65535; v >= bt && v >= 0; --v) ns += hist[(size_t)v];
+    for (long long v = 255; v >= bt && v >= 0; --v) ns += hist[(size_t)v];  // bt > 255: no split
     if (ns * (long long)spp >= (1LL << 30)) ns = 0;
     c->n_split = (unsigned long long)ns;
     c->split_state = ns > 0 ? 0 : -1;
     c->order_ok = false;
     c->rest_n = items - ns;
     c->rest_gt.assign(kOrderKeys, 0u);
-    for (long long b = 0; b < bt && b < 65536; ++b) {  // the unsplit buckets
+    for (long long b = 0; b < bt && b < 256; ++b) {  // the unsplit buckets
       const long long key = std::min(256LL, (b << shift) + ((1LL << shift) >> 1));
       for (long long v = 0; v < key; ++v) c->rest_gt[(size_t)v] += (unsigned)hist[(size_t)b];
     }
@@ -2821,6 +2877,7 @@ int rt_ctx_destroy(rt_ctx* c) {
   if (c->ckpt) (void)hipFree(c->ckpt);
   if (c->order) (void)hipFree(c->order);
   if (c->order_tab) (void)hipFree(c->order_tab);
+  if (c->sort_scratch) (void)hipFree(c->sort_scratch);
   if (c->contrib) (void)hipFree(c->contrib);
   if (c->cam_st) (void)hipFree(c->cam_st);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -3287,33 +3344,15 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
           HIPCHK(c, hipMalloc((void**)&c->order, (size_t)total * sizeof(uint32_t)));
           c->order_cap = total;
         }
-        constexpr int kTab = 256 + 2 * kOrderKeys;  // then the key totals (256)
-        if (!c->order_tab) HIPCHK(c, hipMalloc((void**)&c->order_tab, (size_t)(kTab + 256) * sizeof(unsigned)));
-        // scratch in contrib (12 B per sample; this launch writes it only later): the lengths
-        // (1 B per sample), then the per-tile histograms / offsets (1 KB per 4096 samples)
-        const unsigned tiles = (unsigned)((need + kOrderTile - 1) / kOrderTile);
-        const long long scratch = ((need + 255) & ~255LL) + (long long)tiles * 256 * 4;
-        if (scratch > 4 * c->contrib_cap) {  // tiny splits: 12 B per sample is less than one tile's table
-          if (c->contrib) HIPCHK(c, hipFree(c->contrib));
-          c->contrib = nullptr;
-          c->contrib_cap = 0;
-          HIPCHK(c, hipMalloc((void**)&c->contrib, (size_t)scratch));
-          c->contrib_cap = scratch / 4;
-        }
-        uint8_t* len = (uint8_t*)c->contrib;
-        unsigned* tile_hist = (unsigned*)(len + ((need + 255) & ~255LL));
+        uint8_t* len = sort_keys(c, need);
+        if (!len) return fail(c, RT_ERR_HIP, "out of device memory (split order)");
         split_len_kernel<<<(unsigned)((need + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
             c->ckpt, (unsigned long long)need, a->spp, len);
         HIPCHK(c, hipGetLastError());
-        order_tile_hist_kernel<<<tiles, 64, 0, c->stream>>>(len, (unsigned long long)need, tile_hist);
-        HIPCHK(c, hipGetLastError());
-        order_scan_kernel<<<256, 256, 0, c->stream>>>(tile_hist, tiles, c->order_tab + kTab);
-        HIPCHK(c, hipGetLastError());
         unsigned hist[256];
-        HIPCHK(c, hipMemcpyAsync(hist, c->order_tab + kTab, sizeof(hist), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if ((rc = sort_hist(c, need, hist))) return rc;
         std::vector<unsigned>& t = c->order_tab_host;
-        t.assign(kTab, 0u);
+        t.assign(256 + 2 * kOrderKeys, 0u);
         unsigned* sub_base = t.data();
         unsigned* sub_ge = t.data() + 256;
         unsigned* rest_gt = t.data() + 256 + kOrderKeys;
@@ -3321,8 +3360,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
         for (int v = 0; v < 256; ++v) sub_base[v] = c->rest_gt[(size_t)v] + sub_ge[v + 1];
         std::copy(c->rest_gt.begin(), c->rest_gt.end(), rest_gt);
         HIPCHK(c, hipMemcpyAsync(c->order_tab, t.data(), t.size() * sizeof(unsigned), hipMemcpyHostToDevice, c->stream));
-        order_scatter_kernel<<<tiles, 64, 0, c->stream>>>(len, (unsigned long long)need, tile_hist, c->order_tab, c->order);
-        HIPCHK(c, hipGetLastError());
+        if ((rc = sort_scatter(c, need, c->order_tab, c->order))) return rc;
         if (rest > 0) {
           order_rest_kernel<<<(unsigned)((rest + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
               (unsigned long long)need, (unsigned long long)rest, c->order_tab, c->order);
