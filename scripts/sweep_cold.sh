@@ -1,8 +1,10 @@
 #!/bin/bash
-# Cold-draw priority threshold sweep (RT_COLD_LONG_SEGS) with diag_scale.py's cold columns.
+# Cold-draw sweep of one tuning variable ($VAR, values $VALS) with diag_scale.py's cold columns,
+# C2 10 x 10 and 1 x 100.
 mkdir -p gpurun_out
+VAR=${VAR:-RT_HOT_SEGS_PER_SAMPLE}; VALS=${VALS:-0 2 4 8}
 o=gpurun_out/sweep_cold.log; : > $o
-one() { echo "== RT_COLD_LONG_SEGS=$1 ${*:2}" >> $o; RT_COLD_LONG_SEGS=$1 timeout -k 10 300 python scripts/diag_scale.py "${@:2}" 2>/dev/null | grep "N=" >> $o || exit 1; }
-one 0 && one 20 && one 40 && one 80 &&
-one 0 big1 1200 800 100 1 && one 200 big1 1200 800 100 1 && one 400 big1 1200 800 100 1 && one 800 big1 1200 800 100 1
+one() { echo "== $VAR=$1 ${*:2}" >> $o; env $VAR=$1 timeout -k 10 300 python scripts/diag_scale.py "${@:2}" 2>/dev/null | grep "N=" >> $o || exit 1; }
+for v in $VALS; do one $v || exit 1; done
+for v in $VALS; do one $v big1 1200 800 100 1 || exit 1; done
 cat $o
