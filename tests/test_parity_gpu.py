@@ -72,7 +72,9 @@ VARIANT_MODES = [  # every compiled kernel family, forced to its widest variant 
 ]
 
 
-@pytest.mark.parametrize("scene,W,H,spp,fb_first,fb_count,cam", SMALL)
+@pytest.mark.parametrize("scene,W,H,spp,fb_first,fb_count,cam", SMALL + [
+    ("cornell_smoke", 200, 200, 4, 0, 1, REF),  # the round-2 ray-copy fault's scene, larger
+])
 def test_widest_variants_bit_exact(rtlib, gpu_ctx, oracle, scene, W, H, spp, fb_first, fb_count, cam):
     """The catch-all kernel variants must give the same pixels as the narrow ones a scene gets."""
     import torch
