@@ -153,7 +153,23 @@ constexpr int kStackDepth = 16;
 // lane-interleaved (word k of thread t at [k * block + t]), instead of VGPRs: it is touched once
 // per sample, and without it the variants' live state spills to scratch inside the traversal
 // loops (F_FINAL: 744 B per lane, ~340 B of scratch stores per segment, missing L2).
-constexpr int kLocker = 5;
+constexpr int kLocker = 21;  // words 15..20: the lane's RNG state, lane-contiguous (6 words per lane)
+constexpr int kLockerSmall = 5;  // variants that park only the sample sum, fb and row
+// Variants that also park the per-segment state (locker words 5..20: column, row, sample, depth,
+// counts, attenuation, RNG state): the widest global-memory variants, whose world query spills to
+// scratch at the 4-wave floor.  C5 F_FINAL at 3840x2159 4x4 (MI355X): 86.0 ms with 200 B of
+// scratch per lane; 81.6 ms with words 5..14 parked (140 B); 80.7 ms with the RNG state too (132 B).
+// F_CORNELL (no spills) ran 1 % slower with words 5..14 parked, so it keeps the small locker.
+constexpr bool parks_segment_mask(int mask) {
+  return (mask & F_LDS) == 0 && ((mask & F_ALL) == F_FINAL || (mask & F_ALL) == F_ALL);
+}
+constexpr int locker_words(int mask) { return parks_segment_mask(mask) ? kLocker : kLockerSmall; }
+// Word k of the locker as a T lvalue for parking variants, else the register copy `reg`.
+template <bool PK, typename T>
+__device__ __forceinline__ T& cold_ref(T& reg, uint32_t* slot) {
+  if constexpr (PK) return *reinterpret_cast<T*>(slot);
+  else return reg;
+}
 template <int F>
 constexpr bool parks() {
   return (F & F_LDS) == 0;
@@ -1478,20 +1494,53 @@ void render_kernel(const RenderParams P) {
 #endif
   long long item = -1;  // -1: idle
   bool done = false;
-  int f = 0, i = 0, r = 0, j = 0, s = 0, depth = 0;
-  Rng loc{};
+  // cold state in the LDS locker (parks<F>): 0..2 sample sum, 3 fb, 4 owned row, 5 column,
+  // 6 image row, 7 sample, 8 depth, 9 item segments, 10/11 segment / sample counts, 12..14
+  // attenuation -- touched once per segment or sample, so none of it is live in VGPRs across
+  // the world query (where the widest variants otherwise spill to scratch)
+  uint32_t* const lk = locker_of<F>();
+  constexpr int LB = render_block<F>();
+  constexpr bool PK = parks_segment_mask(F);
+  int f = 0, r = 0;
+  int i_r = 0, j_r = 0, s_r = 0, depth_r = 0;
+  unsigned item_segs_r = 0, nseg_r = 0, nsamp_r = 0;
+  int& i = cold_ref<PK>(i_r, lk + 5 * LB);
+  int& j = cold_ref<PK>(j_r, lk + 6 * LB);
+  int& s = cold_ref<PK>(s_r, lk + 7 * LB);
+  int& depth = cold_ref<PK>(depth_r, lk + 8 * LB);
+  unsigned& item_segs = cold_ref<PK>(item_segs_r, lk + 9 * LB);
+  unsigned& nseg = cold_ref<PK>(nseg_r, lk + 10 * LB);
+  unsigned& nsamp = cold_ref<PK>(nsamp_r, lk + 11 * LB);
+  if constexpr (PK) {
+    nseg = 0;
+    nsamp = 0;
+  }
+  float* const lkf = reinterpret_cast<float*>(lk);
+  V att_r = mk(1, 1, 1);
+  auto att_get = [&]() -> V {
+    if constexpr (PK) return mk(lkf[12 * LB], lkf[13 * LB], lkf[14 * LB]);
+    else return att_r;
+  };
+  auto att_set = [&](V a) {
+    if constexpr (PK) {
+      lkf[12 * LB] = a.x;
+      lkf[13 * LB] = a.y;
+      lkf[14 * LB] = a.z;
+    } else {
+      att_r = a;
+    }
+  };
+  // the RNG state: parked too; the world query (media draws) uses it in place, the camera ray and
+  // scatter on a register copy
+  Rng loc_r{};
+  Rng& loc = cold_ref<PK>(loc_r, (uint32_t*)rt_lds + LB * (kStackDepth + 15) + 6 * threadIdx.x);
   Ray ray{};
-  V att = mk(1, 1, 1), col = mk(0, 0, 0);
-  unsigned nseg = 0, nsamp = 0;
-  unsigned item_segs = 0;
+  V col = mk(0, 0, 0);
   unsigned nnode = 0, nprim = 0, nfall = 0;
   const bool per_pixel = P.cam_mode == RT_CAM_PER_PIXEL;
   const rt_camera& C = S.cam;
   unsigned long long chunk_base = 0;  // wave-uniform: next unclaimed item of the wave's chunk
   unsigned chunk_left = 0;
-  // cold state in the LDS locker (parks<F>): 0..2 sample sum, 3 fb, 4 owned row
-  uint32_t* const lk = locker_of<F>();
-  constexpr int LB = render_block<F>();
 
   for (;;) {
     // ---- refill idle lanes (one atomic per wave, ballot-compacted ranks)
@@ -1542,8 +1591,12 @@ void render_kernel(const RenderParams P) {
       // ---- begin a sample: jitter + camera ray (render.h:105-108, camera.h:49-58)
       if (depth == 0) {
         RT_STAMP(1);
-        camera_ray(P, C, i, j, s, per_pixel, loc, ray);
-        att = mk(1.0f, 1.0f, 1.0f);
+        {
+          Rng lr = loc;
+          camera_ray(P, C, i, j, s, per_pixel, lr, ray);
+          loc = lr;
+        }
+        att_set(mk(1.0f, 1.0f, 1.0f));
       }
 
       // ---- one segment (render.h:60-77)
@@ -1575,18 +1628,21 @@ void render_kernel(const RenderParams P) {
       }
   #endif
       if (!hit_any) {
-        contrib = att * ld3(S.bg);
+        contrib = att_get() * ld3(S.bg);
         ended = true;
       } else {
         V a, em;
-        if (scatter<F>(S, ray, h, a, em, loc)) {
-          att = att * a;
+        Rng lr = loc;
+        const bool sc_ok = scatter<F>(S, ray, h, a, em, lr);
+        loc = lr;
+        if (sc_ok) {
+          att_set(att_get() * a);
           if (++depth == P.max_depth) {
             contrib = mk(0.0f, 0.0f, 0.0f);
             ended = true;
           }
         } else {
-          contrib = att * em;
+          contrib = att_get() * em;
           ended = true;
         }
       }
@@ -2847,7 +2903,7 @@ int rt_ctx_create(int hip_device, rt_ctx** out) {
     for (int v = 0; v < kNumVariants; ++v)
       chk(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->blocks_per_cu[v], kVariants[v].fn, variant_block(v),
                                                        (kVariants[v].mask & F_LDS) ? kLdsBudget
-                                                                                   : variant_block(v) * (kStackDepth + kLocker) * 4),
+                                                                                   : variant_block(v) * (kStackDepth + locker_words(kVariants[v].mask)) * 4),
           "occupancy");
   }
   if (rc != RT_OK) {
@@ -3394,7 +3450,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   P.S.lds_prims = lds_var ? c->dev_prims : 0;
   P.S.lds_mats = lds_var ? c->dev_mats : 0;
   P.S.lds_texs = lds_var ? c->dev_texs : 0;
-  const size_t shmem = lds_var ? lds_bytes + (size_t)bs * kStackDepth * 2 : (size_t)bs * (kStackDepth + kLocker) * 4;
+  const size_t shmem = lds_var ? lds_bytes + (size_t)bs * kStackDepth * 2 : (size_t)bs * (kStackDepth + locker_words(kVariants[var].mask)) * 4;
   // Camera-ray culling, built once per (scene, W, H): candidate lists for the stepwise kernel
   // (world = one BVH), top-level entry masks for list worlds.  Not in the exact / audit modes,
   // whose counters are the reference's.
