@@ -1123,13 +1123,9 @@ __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray&
       return hit;
     }
     if (!hit) return false;
-    // the medium's record again (an opaque index: not kept live in VGPRs across the leaf query)
-    int oi2 = oi;
-    asm volatile("" : "+v"(oi2));
-    const rt_object o2 = S.objects[oi2];
-    if (phase == 1) return medium_hit<F>(o2, r, tmin, tmax, t1, tq, rng, t, prim);
+    if (phase == 1) return medium_hit<F>(o, r, tmin, tmax, t1, tq, rng, t, prim);
     t1 = tq;
-    if (sphere_boundary_no_hit<F>(S, o2.a, t1)) return false;
+    if (sphere_boundary_no_hit<F>(S, o.a, t1)) return false;
     lo = t1 + 0.0001f;
     phase = 1;
   }
