@@ -103,7 +103,10 @@ def parse():
                     help="--gpus N without a launcher: ncclGather over distinct devices, or host copies (ranks may share a GPU)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="debug: gloo runs the N>1 path with host-side collectives and ranks sharing the visible GPUs")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.steps < 1 or a.warmup < 0 or a.cold_steps < 0 or a.gpus < 1:
+        ap.error("--steps and --gpus must be >= 1, --warmup and --cold-steps >= 0")
+    return a
 
 
 CONFIG_OF = {"big1": "C2", "random": "C2", "cornell_smoke": "C3", "door": "C4", "final": "C5"}

@@ -1123,9 +1123,13 @@ __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray&
       return hit;
     }
     if (!hit) return false;
-    if (phase == 1) return medium_hit<F>(o, r, tmin, tmax, t1, tq, rng, t, prim);
+    // the medium's record again (an opaque index: not kept live in VGPRs across the leaf query)
+    int oi2 = oi;
+    asm volatile("" : "+v"(oi2));
+    const rt_object o2 = S.objects[oi2];
+    if (phase == 1) return medium_hit<F>(o2, r, tmin, tmax, t1, tq, rng, t, prim);
     t1 = tq;
-    if (sphere_boundary_no_hit<F>(S, o.a, t1)) return false;
+    if (sphere_boundary_no_hit<F>(S, o2.a, t1)) return false;
     lo = t1 + 0.0001f;
     phase = 1;
   }
@@ -2203,6 +2207,16 @@ __global__ __launch_bounds__(kBlock) void cost_key_kernel(const uint16_t* __rest
   const unsigned long long k = (unsigned long long)blockIdx.x * kBlock + threadIdx.x;
   if (k < n) key[k] = (uint8_t)min(255u, (unsigned)cost[k] >> shift);
 }
+// Largest measured item cost (build_schedule sizes the cost buckets from it).
+__global__ __launch_bounds__(kBlock) void cost_max_kernel(const uint16_t* __restrict__ cost, unsigned long long n,
+                                                          unsigned* __restrict__ out) {
+  unsigned m = 0;
+  for (unsigned long long k = (unsigned long long)blockIdx.x * kBlock + threadIdx.x; k < n;
+       k += (unsigned long long)gridDim.x * kBlock)
+    m = max(m, (unsigned)cost[k]);
+  for (int off = 32; off > 0; off >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, off, 64));
+  if (__lane_id() == 0) atomicMax(out, m);
+}
 __global__ __launch_bounds__(kBlock) void order_rest_kernel(unsigned long long need, unsigned long long rest,
                                                             const unsigned* __restrict__ tab, uint32_t* __restrict__ order) {
   const unsigned long long r = (unsigned long long)blockIdx.x * kBlock + threadIdx.x;
@@ -2777,10 +2791,23 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
   // inside a bucket (a stable counting sort on the device; the top bucket 255 holds every item of
   // >= 2040 segments); the top ~2 % by cost are the "long" prefix whose waves run at raised
   // priority.  (C2, one GPU as rank 0 of N: N = 8 share 3.89 -> 3.45 ms, N = 1 unchanged.)
-  int shift = 3;
-  if (const char* e = getenv("RT_COST_SHIFT")) shift = std::max(0, std::min(12, atoi(e)));  // tuning
+  // Buckets of 8 segments unless the longest item would saturate the top bucket (>= 2040 segments:
+  // high spp); then wider buckets, so the longest items stay ordered and splittable.
   uint8_t* keys = sort_keys(c, items);
   if (!keys) return fail(c, RT_ERR_HIP, "out of device memory (schedule sort)");
+  unsigned cmax = 0;
+  {
+    unsigned* dmax = c->order_tab + 256 + 2 * kOrderKeys;  // key-total words, free until sort_hist
+    HIPCHK(c, hipMemsetAsync(dmax, 0, sizeof(unsigned), c->stream));
+    cost_max_kernel<<<(unsigned)std::min<long long>(1024, (items + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
+        c->item_cost, (unsigned long long)items, dmax);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(&cmax, dmax, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  int shift = 3;
+  while (shift < 8 && (cmax >> shift) > 255u) ++shift;
+  if (const char* e = getenv("RT_COST_SHIFT")) shift = std::max(0, std::min(12, atoi(e)));  // tuning
   cost_key_kernel<<<(unsigned)((items + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
       c->item_cost, (unsigned long long)items, shift, keys);
   HIPCHK(c, hipGetLastError());

@@ -238,7 +238,10 @@ int rt_multi_draw(rt_multi* m, const rt_render_args* args, uint8_t* png_rgb_host
   run_ranks(m, [&](int r) {
     const double a = now_ms();
     rt_ctx* c = m->ctx[r];
-    if (rows[r].empty()) return;
+    if (rows[r].empty()) {  // nothing to render: its (ignored) gather slot is zeros, not stale bytes
+      status[r] = hipMemset(m->rows8[r], 0, padded) == hipSuccess ? RT_OK : RT_ERR_HIP;
+      return;
+    }
     int rc = rt_render_init(c, W, H, args->seed);
     if (!rc) rc = rt_render(c, &ra[r], m->fb[r], &cnt[r]);
     if (!rc) {

@@ -8,4 +8,4 @@ rc=$?
 tail -3 gpurun_out/tests.log
 echo "tests rc=$rc"
 case $rc in 0) ;; *) exit $rc;; esac
-bash scripts/ab_env.sh < ${AB_LIST:-scripts/ab_list.txt}
+bash scripts/ab_env.sh < "${AB_LIST:?set AB_LIST to a file of A/B lines (scripts/ab_env.sh)}"

@@ -1,0 +1,182 @@
+"""GPU parity of multi-GPU shares on the list-world kernel (render_kernel): the shapes C3 and C5 run
+in as ranks of a multi-GPU draw.
+
+A rank owns the 4-row bands b with b % N == rank (rt_owned_rows; band_first = rank, band_stride =
+N).  Pixel results depend only on global indices -- the RNG slot ((id+1) p + id+1) mod W*H and
+curand_init(1984, slot, 0), render.h:91,101 -- so every owned row must equal the oracle's full-frame
+row bit for bit, on the cold launch and on the scheduled (longest-first) launches that follow it.
+Share-size dependent paths exercised here: the camera-ray entry masks of list worlds
+(bin_masks_kernel), the item schedule of a small share, and the step kernel's camera-list threshold
+(RT_BINS_MIN_ITEMS_PER_LANE) on both sides of its switch.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REF = 0
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _assets(scene, tex_shape):
+    """(product scene kwargs, oracle scene kwargs): the door mesh fixture and a synthetic texture of
+    the real file's shape (the reference's files are not on a GPU box)."""
+    from raytracing_gpu_amd import assets
+
+    if scene not in ("final", "door"):
+        return {}, {}
+    m = assets.door_mesh_from_fixture(os.path.join(GOLD, "door_assimp.npz"))
+    img = assets.synthetic_image(*tex_shape)
+    return dict(images=[img], meshes=[m]), dict(images=[img], meshes=[(m.tris, True, 0)])
+
+
+def _share(rtlib, ctx, W, H, spp, nfb, band, launches, kernel_prefix):
+    """Render one rank's share `launches` times (cold, then scheduled); returns the last frame buffer
+    as [nfb, owned rows, W, 3], the owned rows, and every launch's counters and schedule bits."""
+    import torch
+
+    args = rtlib.make_args(W, H, spp, 0, nfb, 50, REF, band_rows=band[0], band_first=band[1], band_stride=band[2])
+    rows = rtlib.owned_rows(args)
+    got, log = None, []
+    for _ in range(launches):
+        ctx.render_init(W, H, 1984)
+        fb = torch.full((nfb * len(rows) * W * 3,), float("nan"), dtype=torch.float32, device="cuda")
+        cnt = ctx.render(args, fb.data_ptr())
+        assert ctx.last_render_kernel().startswith(kernel_prefix), ctx.last_render_kernel()
+        log.append((cnt, ctx.last_render_schedule()))
+        g = fb.cpu().numpy().reshape(nfb, len(rows), W, 3)
+        if got is not None:  # every launch of the share gives the same bits
+            assert np.array_equal(_bits(g), _bits(got))
+        got = g
+    assert not np.isnan(got).any()
+    return got, rows, log
+
+
+@pytest.mark.parametrize("scene", ["cornell_smoke", "final"])
+@pytest.mark.parametrize("n,rank", [(2, 0), (2, 1), (8, 0), (8, 7)])
+def test_list_world_share_every_row(rtlib, gpu_ctx, oracle, scene, n, rank):
+    """640x360 (final) / 200x200 (cornell_smoke), 2 fbs: rank `rank` of `n` against the oracle's full
+    frame on every owned row, on the cold launch and on the two scheduled launches after it."""
+    pa, oa = _assets(scene, (341, 152))
+    W, H, spp, nfb = (640, 360, 1, 2) if scene == "final" else (200, 200, 2, 2)
+    gpu_ctx.upload(rtlib.Scene.builtin(scene, **pa))
+    got, rows, log = _share(rtlib, gpu_ctx, W, H, spp, nfb, (4, rank, n), 3, "render_kernel<")
+    assert log[0][1] == 0 and all(s & rtlib.RT_SCHED_PREVIOUS for _, s in log[2:])
+    ref = oracle.RefScene(scene, **oa)
+    segs = 0
+    for f in range(nfb):
+        want, _, per_px = ref.render(W, H, spp, f, 50, REF, seg_per_pixel=True)
+        want = want.reshape(H, W, 3)[rows]
+        segs += int(per_px.reshape(H, W)[rows].sum())
+        diff = (_bits(got[f]) != _bits(want)).any(axis=2)
+        assert not diff.any(), f"{scene} rank {rank}/{n} fb {f}: {int(diff.sum())} pixels differ"
+    for cnt, _ in log:
+        assert cnt["segments"] == segs
+        assert cnt["samples"] == nfb * len(rows) * W * spp
+
+
+@pytest.mark.parametrize("n,rank", [(8, 0), (8, 7), (2, 1)])
+def test_c5_share_full_size(rtlib, gpu_ctx, oracle, n, rank):
+    """C5 as one rank of its 8-GPU tiling: final at 3840x2159, 1 spp, 2 fbs; the share rendered whole
+    on the GPU (cold, then scheduled), an owned-row subset against the oracle."""
+    pa, oa = _assets("final", (3410, 1518))
+    W, H, spp, nfb = 3840, 2159, 1, 2
+    gpu_ctx.upload(rtlib.Scene.builtin("final", **pa))
+    got, rows, _ = _share(rtlib, gpu_ctx, W, H, spp, nfb, (4, rank, n), 2, "render_kernel<")
+    # owned rows 4 b + k with b = rank + N m: the oracle's progression row0 = 4 rank + 1, step 4 N * 9
+    sub = (4 * rank + 1, 4 * n * 9)
+    js = list(range(sub[0], H, sub[1]))
+    pos = {int(j): q for q, j in enumerate(rows)}
+    assert all(j in pos for j in js)
+    ref = oracle.RefScene("final", **oa)
+    for f in range(nfb):
+        want = ref.render(W, H, spp, f, 50, REF, rows=sub)[0].reshape(H, W, 3)
+        q = [pos[j] for j in js]
+        assert np.array_equal(_bits(got[f][q]), _bits(want[js])), f"C5 rank {rank}/{n} fb {f}"
+
+
+@pytest.mark.parametrize("threshold", [None, "0", "1e9"], ids=["default", "lists", "traverse"])
+@pytest.mark.parametrize("n", [4, 8])
+def test_step_share_across_camera_list_switch(rtlib, gpu_ctx, oracle, monkeypatch, n, threshold):
+    """C2's 10-fb workload as rank N-1 of N = 4 (9.2 items per resident lane: camera lists on at the
+    product's threshold of 6) and N = 8 (4.6: off), 1 spp per fb; also forced on and off.  Cold and
+    scheduled launches against the oracle on an owned-row subset."""
+    if threshold is None:
+        monkeypatch.delenv("RT_BINS_MIN_ITEMS_PER_LANE", raising=False)
+    else:
+        monkeypatch.setenv("RT_BINS_MIN_ITEMS_PER_LANE", threshold)
+    W, H, spp, nfb = 1200, 800, 1, 10
+    rank = n - 1
+    gpu_ctx.upload(rtlib.Scene.builtin("big1"))
+    got, rows, _ = _share(rtlib, gpu_ctx, W, H, spp, nfb, (4, rank, n), 3, "render_step_kernel<")
+    sub = (4 * rank + 2, 4 * n * 7)
+    js = list(range(sub[0], H, sub[1]))
+    pos = {int(j): q for q, j in enumerate(rows)}
+    ref = oracle.RefScene("big1")
+    for f in range(nfb):
+        want = ref.render(W, H, spp, f, 50, REF, rows=sub)[0].reshape(H, W, 3)
+        q = [pos[j] for j in js]
+        assert np.array_equal(_bits(got[f][q]), _bits(want[js])), f"big1 rank {rank}/{n} fb {f}"
+
+
+@pytest.mark.parametrize("ranks", [2, 8])
+def test_multi_draw_final_matches_draw(rtlib, ranks):
+    """rt_multi_draw (include/rt_multi.h) of C5's scene over `ranks` ranks sharing the box's GPU
+    (host gather): the assembled image is byte-identical to the single-context rt_draw, on the cold
+    draw and on the warm draws after it."""
+    from raytracing_gpu_amd import multi
+
+    pa, _ = _assets("final", (341, 152))
+    sc = rtlib.Scene.builtin("final", **pa)
+    W, H, spp, nfb = 320, 180, 2, 2
+    args = rtlib.make_args(W, H, spp, 0, nfb, 50, REF, band_rows=4)
+    ctx = rtlib.Context(0)
+    try:
+        ctx.upload(sc)
+        want, cw = ctx.draw_args(args)
+    finally:
+        ctx.close()
+    m = multi.Multi([0] * ranks, multi.RT_GATHER_HOST)
+    try:
+        m.upload(sc)
+        for k in range(3):
+            img, cnt, tm = m.draw(args)
+            assert np.array_equal(img, want), f"draw {k}"
+            assert cnt["segments"] == cw["segments"]
+            assert tm["warm"] == (0 if k == 0 else 1)
+    finally:
+        m.close()
+
+
+def test_multi_rccl_one_rank_matches_draw(rtlib):
+    """The RCCL gather path of rt_multi (ncclCommInitAll, ncclGather inside a group, stream drain)
+    with one rank on the box's device: the image equals rt_draw byte for byte, the gather moved the
+    padded rows, and `warm` is 0 on the first draw of a configuration and 1 on its repeats."""
+    from raytracing_gpu_amd import multi
+
+    sc = rtlib.Scene.builtin("big1")
+    W, H, spp, nfb = 160, 90, 2, 3
+    args = rtlib.make_args(W, H, spp, 0, nfb, 50, REF, band_rows=4)
+    ctx = rtlib.Context(0)
+    try:
+        ctx.upload(sc)
+        want, cw = ctx.draw_args(args)
+    finally:
+        ctx.close()
+    m = multi.Multi([0], multi.RT_GATHER_RCCL)
+    try:
+        m.upload(sc)
+        for k in range(3):
+            img, cnt, tm = m.draw(args)
+            assert np.array_equal(img, want), f"draw {k}"
+            assert cnt["segments"] == cw["segments"]
+            assert tm["gather_bytes"] == H * W * 3
+            assert tm["warm"] == (0 if k == 0 else 1)
+    finally:
+        m.close()
