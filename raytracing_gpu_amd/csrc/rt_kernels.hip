@@ -40,6 +40,8 @@
 #define RT_PRIM_TYPE_MASK 0xff
 #define RT_PRIM_FLAG_UV 0x100      // material needs sphere u,v (image texture)
 #define RT_PRIM_FLAG_UNIT_T 0x200  // moving sphere with time0 = 0, time1 - time0 = 1
+#define RT_PRIM_FLAG_XF 0x400      // world-tree leaf under a translate/rotate_y instance (F_WORLD)
+#define RT_WKEY_SHIFT 20           // world-tree tie key: (n_world - 1 - entry) << 20 | reference leaf rank
 
 // Scene feature mask: the render kernel is instantiated per feature set so that a scene pays
 // registers only for the primitive / object / texture kinds it contains.
@@ -59,6 +61,8 @@ enum : int {
   F_CHECK = 1 << 12,  // culled search + exact re-run per query; disagreements logged (audit mode)
   F_LDS = 1 << 13,    // BVH nodes + primitives staged in LDS (1024-thread workgroups, 1 per CU)
   F_STEP = 1 << 14,   // world = one BVH object: render_step_kernel (one traversal step per loop trip)
+  F_WORLD = 1 << 15,  // list world flattened into ONE traversal tree (render_step_kernel; rt_scene_upload)
+  F_QLDS = 1 << 16,   // the world BVH's traversal tree quantized to 24-byte pair records in LDS (qpair)
   F_ALL = (1 << 11) - 2,
   F_SPHERES = F_MOVING | F_CHECKER | F_BVH,           // basic, first, big1 (C2), two_spheres
   F_CORNELL = F_RECT | F_LIST | F_XFORM | F_MEDIUM,   // cornell, cornell_smoke (C3)
@@ -90,6 +94,22 @@ struct DScene {
   int32_t lds_mats;      // F_LDS: materials staged after the margins (one float4 each)
   int32_t lds_texs;      // F_LDS: textures staged after the materials (two float4 each; stacks follow)
   const float4* cam_tab; // REF camera mode: lens offset (xyz) and time (w) of sample s (camera_ray)
+  // F_WORLD (list world as one traversal tree, see build_world_tree): 4 float4 per leaf -- the
+  // primitive's record (c.y = tie key, RT_PRIM_FLAG_XF in the type word for instance members) and
+  // {instance, world entry, reference BVH object or -1, primitive} as ints; 2 float4 per instance
+  // {translate xyz, flags bits} {sin, cos}; world entries from w_media on are constant media queried
+  // in list order after the tree; w_inert: inert sphere-bounded media sit between tree entries.
+  const float4* wleaf;
+  const float4* wxf;
+  int32_t wt_fb;
+  int32_t w_media;
+  int32_t w_inert;
+  int32_t pad_w;
+  // F_QLDS: the world BVH's traversal tree as 24-byte pair records (build_qtree), staged in LDS;
+  // q_ebias: exponent bias of their 5-bit per-axis scales
+  const uint32_t* qnodes;
+  int32_t q_pairs;
+  int32_t q_ebias;
   rt_camera cam;
   float bg[3];
 };
@@ -112,7 +132,7 @@ __device__ __forceinline__ const float4* prims_of(const DScene& S) {
 }
 template <int F>
 constexpr int render_block() {
-  return (F & F_LDS) != 0 ? 1024 : 256;
+  return (F & (F_LDS | F_QLDS)) != 0 ? 1024 : 256;
 }
 // Validation margins (F_LDS: staged after the primitives, two per float4).
 template <int F>
@@ -138,11 +158,13 @@ __device__ __forceinline__ const rt_texture* texs_of(const DScene& S) {
 // Stack entries: child words (pair index, or -1 - primitive).  F_LDS scenes have < 32768 pairs and
 // primitives (they fit in LDS), so their entries are 16-bit (32 KB of stacks per 1024 lanes).
 template <int F>
-using stack_t = std::conditional_t<(F & F_LDS) != 0, short, int>;
+using stack_t = std::conditional_t<(F & (F_LDS | F_QLDS)) != 0, short, int>;
 template <int F>
 __device__ __forceinline__ stack_t<F>* stack_of(const DScene& S) {
   if constexpr ((F & F_LDS) != 0)
     return (short*)(rt_lds + lds_mats_at(S) + S.lds_mats + 2 * S.lds_texs) + threadIdx.x;
+  else if constexpr ((F & F_QLDS) != 0)
+    return (short*)((uint32_t*)rt_lds + 6 * S.q_pairs) + threadIdx.x;
   else return (int*)rt_lds + threadIdx.x;
 }
 // Per-lane traversal stack in LDS (after the staged scene for F_LDS variants), lane-interleaved
@@ -161,9 +183,12 @@ constexpr int kLockerSmall = 5;  // variants that park only the sample sum, fb a
 // scratch per lane; 81.6 ms with words 5..14 parked (140 B); 80.7 ms with the RNG state too (132 B).
 // F_CORNELL (no spills) ran 1 % slower with words 5..14 parked, so it keeps the small locker.
 constexpr bool parks_segment_mask(int mask) {
-  return (mask & F_LDS) == 0 && ((mask & F_ALL) == F_FINAL || (mask & F_ALL) == F_ALL);
+  return (mask & (F_LDS | F_STEP)) == 0 && ((mask & F_ALL) == F_FINAL || (mask & F_ALL) == F_ALL);
 }
-constexpr int locker_words(int mask) { return parks_segment_mask(mask) ? kLocker : kLockerSmall; }
+// (render_step_kernel keeps no locker: only its traversal stack is in LDS)
+constexpr int locker_words(int mask) {
+  return (mask & F_STEP) != 0 ? 0 : (parks_segment_mask(mask) ? kLocker : kLockerSmall);
+}
 // Word k of the locker as a T lvalue for parking variants, else the register copy `reg`.
 template <bool PK, typename T>
 __device__ __forceinline__ T& cold_ref(T& reg, uint32_t* slot) {
@@ -266,6 +291,24 @@ struct Hit {
 __device__ __forceinline__ void set_face(Hit& h, const Ray& r, V out) {  // hittable.h:17-22
   h.front = dot(r.d, out) < 0;
   h.n = h.front ? out : neg(out);
+}
+
+// translate(rotate_y(child)) ray into the child's frame (hittable.h:37-59, 112-143), from an
+// instance record {translate xyz, flags bits} {sin, cos} (flags: 1 translate, 2 rotate_y); the same
+// float operations as xform_ray on the rt_object.  moved = the ray after the translation only.
+__device__ __forceinline__ Ray xform_ray_x(float4 x0, float4 x1, const Ray& r, Ray& moved) {
+  const int fl = __float_as_int(x0.w);
+  moved = r;
+  if (fl & 1) moved.o = r.o - mk(x0.x, x0.y, x0.z);
+  Ray rr = moved;
+  if (fl & 2) {
+    const float s = x1.x, c = x1.y;
+    rr.o.x = c * moved.o.x - s * moved.o.z;
+    rr.o.z = s * moved.o.x + c * moved.o.z;
+    rr.d.x = c * moved.d.x - s * moved.d.z;
+    rr.d.z = s * moved.d.x + c * moved.d.z;
+  }
+  return rr;
 }
 
 using Rng = rtx::State;
@@ -652,10 +695,17 @@ __device__ __forceinline__ bool bvh_exact(const DScene& S, int base, int rows, c
 // smaller t, ties to the lower leaf rank), and the loser is not kept in `second`: an exact loser of
 // an exact winner has t >= the winner's t, so when a range later displaces that winner, the
 // winner's lo (added to `second`) covers it.
+// World tree (WORLD, F_WORLD): candidates of different world entries carry different entry parts
+// of the tie key (rk >> RT_WKEY_SHIFT).  An exact candidate of another entry is never dropped from
+// `second`: it bounds the closest-so-far that the reference's list passes to the winner's entry
+// (world_settle), and an exact tie across entries leaves second == bhi, so the query is not certain.
+template <bool WORLD = false>
 __device__ __forceinline__ void take_candidate(float lo, float hi, int pi, int rk, float& blo, float& bhi,
                                                float& second, int& best_prim, int& best_rank) {
   if (lo == hi && blo == bhi) {  // both exact: the reference's rule, ties to the lower rank
+    const bool other = WORLD && (rk >> RT_WKEY_SHIFT) != (best_rank >> RT_WKEY_SHIFT);
     if (lo < blo || (lo == blo && rk < best_rank)) {
+      if (other) second = __builtin_fminf(second, blo);
       blo = lo;
       bhi = hi;
       best_prim = pi;
@@ -672,6 +722,52 @@ __device__ __forceinline__ void take_candidate(float lo, float hi, int pi, int r
   }
 }
 
+// One pair record of the quantized traversal tree (F_QLDS, build_qtree), 6 words in LDS:
+//   w0 = origin x | y (binary16, rounded down), w1 = origin z | (ex | ey << 5 | ez << 10) << 16,
+//   w2..w4 = child 0 lo xyz, hi xyz, child 1 lo xyz, hi xyz as bytes q (box coordinate origin +
+//   q * 2^(e + q_ebias), lo rounded down and hi up from the padded box), w5 = child 0 | child 1 (16-bit
+//   child words: pair index, or -1 - primitive).
+// Slab values t = (origin + q 2^E - o) / d as fma(q, A, B) with A = 2^E finv, B = origin finv - oi per
+// axis: two instructions per axis on top of fbox's one fma per bound.  The quantized boxes contain the
+// padded ones (2^-16 relative), far wider than the few roundings of A, B and the fma.
+__device__ __forceinline__ float q_half(uint32_t bits16) {
+  const uint16_t b = (uint16_t)bits16;
+  _Float16 h;
+  __builtin_memcpy(&h, &b, 2);
+  return (float)h;
+}
+__device__ __forceinline__ float q_byte(uint32_t w, int k) { return (float)((w >> (8 * k)) & 255u); }
+__device__ __forceinline__ bool qbox(float lx, float ly, float lz, float hx, float hy, float hz, V A, V B, float tmin,
+                                     float tcut, float& tn) {
+  const float x0 = __builtin_fmaf(lx, A.x, B.x), x1 = __builtin_fmaf(hx, A.x, B.x);
+  const float y0 = __builtin_fmaf(ly, A.y, B.y), y1 = __builtin_fmaf(hy, A.y, B.y);
+  const float z0 = __builtin_fmaf(lz, A.z, B.z), z1 = __builtin_fmaf(hz, A.z, B.z);
+  const float tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x0, x1), __builtin_fminf(y0, y1)),
+                                      __builtin_fmaxf(__builtin_fminf(z0, z1), tmin));
+  const float tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x0, x1), __builtin_fmaxf(y0, y1)),
+                                     __builtin_fminf(__builtin_fmaxf(z0, z1), tcut));
+  tn = tnear;
+  return tnear <= tfar;
+}
+__device__ __forceinline__ void qpair(const DScene& S, int cur, V oi, V finv, float tmin, float tcut, bool& hl,
+                                      bool& hr, float& tl, float& tr, int& c0, int& c1) {
+  const uint2* rec = reinterpret_cast<const uint2*>((const uint32_t*)rt_lds + 6 * cur);
+  const uint2 a = rec[0], b = rec[1], c = rec[2];
+  const uint32_t ee = a.y >> 16;
+  const V org = mk(q_half(a.x), q_half(a.x >> 16), q_half(a.y));
+  const V sc = mk(__builtin_ldexpf(1.0f, (int)(ee & 31u) + S.q_ebias), __builtin_ldexpf(1.0f, (int)((ee >> 5) & 31u) + S.q_ebias),
+                  __builtin_ldexpf(1.0f, (int)((ee >> 10) & 31u) + S.q_ebias));
+  const V A = mk(sc.x * finv.x, sc.y * finv.y, sc.z * finv.z);
+  const V B = mk(__builtin_fmaf(org.x, finv.x, -oi.x), __builtin_fmaf(org.y, finv.y, -oi.y),
+                 __builtin_fmaf(org.z, finv.z, -oi.z));
+  hl = qbox(q_byte(b.x, 0), q_byte(b.x, 1), q_byte(b.x, 2), q_byte(b.x, 3), q_byte(b.y, 0), q_byte(b.y, 1), A, B,
+            tmin, tcut, tl);
+  hr = qbox(q_byte(b.y, 2), q_byte(b.y, 3), q_byte(c.x, 0), q_byte(c.x, 1), q_byte(c.x, 2), q_byte(c.x, 3), A, B,
+            tmin, tcut, tr);
+  c0 = (int)(short)(c.y & 0xffffu);
+  c1 = (int)(short)(c.y >> 16);
+}
+
 template <int F>
 __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r, V oi, V finv, float a, float rcpa,
                                           float tmin, float tmax, int& cur, int& sp, float& blo, float& bhi,
@@ -680,15 +776,22 @@ __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r,
   stack_t<F>* stk = stack_of<F>(S);
   constexpr int BS = render_block<F>();
   RT_STAMP(3);
-  const float4* n = nodes_of<F>(S) + 2 * (fb + 2 * cur);
-  const float4 l0 = n[0], l1 = n[1], r0 = n[2], r1 = n[3];
   if constexpr ((F & F_STATS) != 0) nnode += 2;
   // bhi >= the winner's exact t: a box entered beyond bhi*(1+2^-8) holds no primitive that can win
   const float cut = __builtin_fminf(bhi * 1.00390625f, tmax);
   float tl, tr;
-  bool hl = fbox(l0, l1, oi, finv, tmin, cut, tl);
-  bool hr = fbox(r0, r1, oi, finv, tmin, cut, tr);
-  const int c0 = __float_as_int(l0.w), c1 = __float_as_int(l1.w);
+  bool hl, hr;
+  int c0, c1;
+  if constexpr ((F & F_QLDS) != 0) {
+    qpair(S, cur, oi, finv, tmin, cut, hl, hr, tl, tr, c0, c1);
+  } else {
+    const float4* n = nodes_of<F>(S) + 2 * (fb + 2 * cur);
+    const float4 l0 = n[0], l1 = n[1], r0 = n[2], r1 = n[3];
+    hl = fbox(l0, l1, oi, finv, tmin, cut, tl);
+    hr = fbox(r0, r1, oi, finv, tmin, cut, tr);
+    c0 = __float_as_int(l0.w);
+    c1 = __float_as_int(l1.w);
+  }
   // Primitive children are tested right away (leaves hold one primitive): one pass for the lanes
   // with a hit leaf child on either side, a second only for lanes with two (the candidate kept does
   // not depend on the order, see take_candidate).  3 % faster on C2 than a pass per side.
@@ -704,10 +807,29 @@ __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r,
       if (ch < 0) {
         RT_STAMP(4);
         const int pi = -ch - 1;
-        const PrimRec q = load_prim<F>(S, pi);
-        float lo, hi;
-        if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim))
-          take_candidate(lo, hi, pi, __float_as_int(q.c.y), blo, bhi, second, best_prim, best_rank);
+        if constexpr ((F & F_WORLD) != 0) {
+          // world-tree leaf: its record, tested in its instance's frame (the reference's ray for
+          // that entry, hittable.h:37-59, 112-143) when it belongs to a translate/rotate_y
+          const float4* L = S.wleaf + 4 * pi;
+          const PrimRec q{L[0], L[1], L[2]};
+          float lo, hi;
+          Ray rr = r;
+          float a2 = a, rc2 = rcpa;
+          if ((F & F_XFORM) != 0 && (__float_as_int(q.c.z) & RT_PRIM_FLAG_XF) != 0) {
+            const int xf = __float_as_int(L[3].x);
+            Ray moved;
+            rr = xform_ray_x(S.wxf[2 * xf], S.wxf[2 * xf + 1], r, moved);
+            a2 = len2(rr.d);
+            rc2 = __builtin_amdgcn_rcpf(a2);
+          }
+          if (prim_range<F>(S, q, rr, a2, rc2, tmin, tmax, lo, hi, nprim))
+            take_candidate<true>(lo, hi, pi, __float_as_int(q.c.y), blo, bhi, second, best_prim, best_rank);
+        } else {
+          const PrimRec q = load_prim<F>(S, pi);
+          float lo, hi;
+          if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim))
+            take_candidate(lo, hi, pi, __float_as_int(q.c.y), blo, bhi, second, best_prim, best_rank);
+        }
         RT_STAMP(3);
       }
     }
@@ -764,49 +886,14 @@ __device__ __forceinline__ void tile_candidates(const DScene& S, const int32_t* 
   }
 }
 
-// Second half of bvh_closest once the candidate search has ended: overflow fallback, audit mode,
-// and the reference-chain validation of the candidate (best_rank = its reference leaf rank).
+// Reference-chain validation of a candidate search's winner (best_prim at exact t = best, reference
+// leaf rank best_rank of the BVH at `base` with `rows` inner levels): true when the reference's
+// visit set certainly reaches it, i.e. every reference ancestor passes the slab test against
+// [tmin, tmax]; false when that is not certain (the caller re-runs the query exactly).
 template <int F>
-__device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, const Ray& r, float tmin, float tmax,
-                                           bool overflow, float bhi, float second, float& best, int& best_prim,
-                                           int best_rank, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+__device__ __forceinline__ bool chain_ok(const DScene& S, int base, int rows, const Ray& r, float tmin, float tmax,
+                                         float best, int best_prim, int best_rank, unsigned& nnode) {
   const int last0 = (1 << (rows - 1)) - 1;
-  // the reference's reciprocals (three IEEE divides), only on the rare paths that test boxes
-  auto inv_of = [&r]() { return mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z); };
-  // The candidate search keeps ranges: its winner is certain when every other candidate's range
-  // lies above the winner's (second > bhi), and its exact t (the reference's hit() value) must
-  // pass [tmin, tmax].  Otherwise -- a subtree dropped on stack overflow, overlapping ranges (near
-  // ties), a range straddling tmin -- the query is answered on the exact visit set.
-  // On entry best = the winner's lo (= its exact t when lo = hi).
-  bool sure = !overflow && (best_prim < 0 || second > bhi);  // no candidate at all: a certain miss
-  if (sure && best_prim >= 0 && best != bhi) {
-    float t;
-    unsigned np = 0;
-    sure = prim_t<F>(S, best_prim, r, tmin, tmax, t, np);
-    best = t;
-  }
-  if (!sure) {
-    if constexpr ((F & F_STATS) != 0) ++nfall;
-    return bvh_exact<F>(S, base, rows, r, inv_of(), tmin, tmax, best, best_prim, nnode, nprim, nfall);
-  }
-  if constexpr ((F & F_CHECK) != 0) {
-    float te;
-    int pe;
-    bvh_exact<F>(S, base, rows, r, inv_of(), tmin, tmax, te, pe, nnode, nprim, nfall);
-    if (pe != best_prim || (pe >= 0 && __float_as_uint(te) != __float_as_uint(best))) {
-      const unsigned slot = atomicAdd(S.dbg_n, 1u);
-      if ((int)slot < S.dbg_cap) {
-        float* e = S.dbg + 16 * slot;
-        e[0] = r.o.x; e[1] = r.o.y; e[2] = r.o.z; e[3] = r.d.x; e[4] = r.d.y; e[5] = r.d.z; e[6] = r.tm;
-        e[7] = tmin; e[8] = tmax; e[9] = best; e[10] = __int_as_float(best_prim); e[11] = te;
-        e[12] = __int_as_float(pe); e[13] = __int_as_float(best_rank); e[14] = 0.0f; e[15] = 0.0f;
-      }
-    }
-    best = te;
-    best_prim = pe;
-    return pe >= 0;
-  }
-  if (best_prim < 0) return false;
   // Reference ancestors whose box contains the winner's box with a margin wider than any
   // displacement of its computed hit point (hit-distance error up to ~4e-4 t for grazing
   // spheres, slab rounding 2^-22 of the distance) cannot reject this ray, so only the other
@@ -869,15 +956,109 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
           __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(hi.x), __builtin_fabsf(hi.y)), __builtin_fabsf(hi.z)));
       const float need = 0x1p-20f * (bmax + obase);
       if (!(__builtin_fminf(__builtin_fminf(mx, my), mz) > need)) {
-        const V inv = inv_of();  // rare: not kept live across the chain
-        if (!box_hit(lo, hi, r, inv, tmin, tmax)) {
-          if constexpr ((F & F_STATS) != 0) ++nfall;
-          return bvh_exact<F>(S, base, rows, r, inv, tmin, tmax, best, best_prim, nnode, nprim, nfall);
-        }
+        // the reference's reciprocals (three IEEE divides), only on this rare path
+        if (!box_hit(lo, hi, r, mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z), tmin, tmax)) return false;
       }
     }
     if (kr == 0) return true;
   }
+}
+
+// Second half of bvh_closest once the candidate search has ended: overflow fallback, audit mode,
+// and the reference-chain validation of the candidate (best_rank = its reference leaf rank).
+template <int F>
+__device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, const Ray& r, float tmin, float tmax,
+                                           bool overflow, float bhi, float second, float& best, int& best_prim,
+                                           int best_rank, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+  // the reference's reciprocals (three IEEE divides), only on the rare paths that test boxes
+  auto inv_of = [&r]() { return mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z); };
+  // The candidate search keeps ranges: its winner is certain when every other candidate's range
+  // lies above the winner's (second > bhi), and its exact t (the reference's hit() value) must
+  // pass [tmin, tmax].  Otherwise -- a subtree dropped on stack overflow, overlapping ranges (near
+  // ties), a range straddling tmin -- the query is answered on the exact visit set.
+  // On entry best = the winner's lo (= its exact t when lo = hi).
+  bool sure = !overflow && (best_prim < 0 || second > bhi);  // no candidate at all: a certain miss
+  if (sure && best_prim >= 0 && best != bhi) {
+    float t;
+    unsigned np = 0;
+    sure = prim_t<F>(S, best_prim, r, tmin, tmax, t, np);
+    best = t;
+  }
+  if (!sure) {
+    if constexpr ((F & F_STATS) != 0) ++nfall;
+    return bvh_exact<F>(S, base, rows, r, inv_of(), tmin, tmax, best, best_prim, nnode, nprim, nfall);
+  }
+  if constexpr ((F & F_CHECK) != 0) {
+    float te;
+    int pe;
+    bvh_exact<F>(S, base, rows, r, inv_of(), tmin, tmax, te, pe, nnode, nprim, nfall);
+    if (pe != best_prim || (pe >= 0 && __float_as_uint(te) != __float_as_uint(best))) {
+      const unsigned slot = atomicAdd(S.dbg_n, 1u);
+      if ((int)slot < S.dbg_cap) {
+        float* e = S.dbg + 16 * slot;
+        e[0] = r.o.x; e[1] = r.o.y; e[2] = r.o.z; e[3] = r.d.x; e[4] = r.d.y; e[5] = r.d.z; e[6] = r.tm;
+        e[7] = tmin; e[8] = tmax; e[9] = best; e[10] = __int_as_float(best_prim); e[11] = te;
+        e[12] = __int_as_float(pe); e[13] = __int_as_float(best_rank); e[14] = 0.0f; e[15] = 0.0f;
+      }
+    }
+    best = te;
+    best_prim = pe;
+    return pe >= 0;
+  }
+  if (best_prim < 0) return false;
+  if (chain_ok<F>(S, base, rows, r, tmin, tmax, best, best_prim, best_rank, nnode)) return true;
+  if constexpr ((F & F_STATS) != 0) ++nfall;
+  return bvh_exact<F>(S, base, rows, r, inv_of(), tmin, tmax, best, best_prim, nnode, nprim, nfall);
+}
+
+// A ray whose sphere tests cannot produce a NaN root against the scene's inert media boundaries
+// (spheres with coordinates and radii below 1e6, checked at upload): finite, |o| < 1e7, 1e-12 <
+// |d|^2 < 1e8 -- then hb^2 and a*cc stay below ~1e23, and root = num / a is finite.  NaN and inf
+// fail the comparisons.
+__device__ __forceinline__ bool ray_sane(const Ray& r) {
+  const float a = len2(r.d);
+  const float om = __builtin_fabsf(r.o.x) + __builtin_fabsf(r.o.y) + __builtin_fabsf(r.o.z) + __builtin_fabsf(r.tm);
+  return a > 1e-12f && a < 1e8f && om < 1e7f;
+}
+
+// Outcome of the world tree's candidate search (F_WORLD; leaf = winning leaf, key its tie key):
+// 0 = certain miss, 1 = certain hit (best = the reference's t; wobj / prim = its world object and
+// primitive), 2 = not certain: the caller answers the query on the reference's sequential list.
+// The reference's list (hittable_list.h:23-39) queries the winner's entry with t_max = the closest
+// hit of the entries before it; that value is at least `lim`: every candidate of another entry lies
+// at or above `second` (take_candidate<true>), and a box culled beyond the cut bhi*(1+2^-8) holds
+// only primitives hit beyond bhi*(1+2^-9).  The winner's reference chain is validated against
+// [tmin, lim]: a slab test that passes there passes for any larger t_max.
+template <int F>
+__device__ __forceinline__ int world_settle(const DScene& S, const Ray& r, float tmin, bool overflow, float bhi,
+                                            float second, float& best, int leaf, int key, int& wobj, int& prim,
+                                            unsigned& nnode) {
+  if (overflow || (leaf >= 0 && !(second > bhi))) return 2;
+  if (leaf < 0) return 0;
+  const float4* L = S.wleaf + 4 * leaf;
+  const PrimRec q{L[0], L[1], L[2]};
+  const float4 dw = L[3];
+  Ray rr = r;
+  if ((F & F_XFORM) != 0 && (__float_as_int(q.c.z) & RT_PRIM_FLAG_XF) != 0) {
+    const int xf = __float_as_int(dw.x);
+    Ray moved;
+    rr = xform_ray_x(S.wxf[2 * xf], S.wxf[2 * xf + 1], r, moved);
+  }
+  if (best != bhi) {  // a range: the exact root once, IEEE sqrt and divide
+    float t;
+    unsigned np = 0;
+    if (!prim_t_q<F>(S, q, rr, tmin, __builtin_inff(), t, np)) return 2;
+    best = t;
+  }
+  const int bobj = __float_as_int(dw.z);
+  prim = __float_as_int(dw.w);
+  if (bobj >= 0) {
+    const int base = S.objects[bobj].a, rows = S.objects[bobj].b;
+    const float lim = __builtin_fminf(second, bhi * 1.0009765625f);
+    if (!chain_ok<F>(S, base, rows, rr, tmin, lim, best, prim, key & ((1 << RT_WKEY_SHIFT) - 1), nnode)) return 2;
+  }
+  wobj = S.world[__float_as_int(dw.y)];
+  return 1;
 }
 
 // Closest primitive of a reference BVH object, same result as bvh_exact.
@@ -1721,6 +1902,11 @@ __global__ __launch_bounds__(render_block<F>()) __attribute__((amdgpu_waves_per_
 void render_step_kernel(const RenderParams P) {
   const DScene& S = P.S;
   if constexpr ((F & F_LDS) != 0) stage_lds<F>(S);  // nodes, primitives, margins, materials, textures
+  if constexpr ((F & F_QLDS) != 0) {  // the quantized traversal tree (24-byte pair records)
+    uint32_t* q = (uint32_t*)rt_lds;
+    for (int k = threadIdx.x; k < 6 * S.q_pairs; k += render_block<F>()) q[k] = S.qnodes[k];
+    __syncthreads();
+  }
   const unsigned lane = __lane_id();
 #ifdef RT_STEP_DIAG
   if (lane < 4) rt_diag_acc[threadIdx.x >> 6][lane] = 0;
@@ -1731,7 +1917,7 @@ void render_step_kernel(const RenderParams P) {
   RT_STAMP(0);
 #endif
   const rt_object obj = S.objects[S.world[0]];
-  const int tbase = obj.c;  // traversal tree of the world's BVH
+  const int tbase = (F & F_WORLD) != 0 ? S.wt_fb : obj.c;  // traversal tree of the world's BVH / the world tree
   const float tmin = 0.001f, tmax = __builtin_inff();  // render.h:63
   long long item = -1;  // -1: no item
   bool done = false;
@@ -1773,25 +1959,75 @@ void render_step_kernel(const RenderParams P) {
         ++item_segs;
         bool ended = false;
         V contrib;
-        bool hit = bvh_settle<F>(S, obj.a, obj.b, ray, tmin, tmax, overflow, bhi, second, best, best_prim, best_rank,
-                                 nnode, nprim, nfall);
-        // primitive objects after the BVH in the world list (C4's ground sphere): hittable_list's
-        // rule, t_max = the closest hit so far (inclusive), so a later entry wins a tie
-        for (int w = 1; w < S.n_world; ++w) {
-          const rt_object po = S.objects[S.world[w]];
-          float tq;
-          if (prim_t<F>(S, po.a, ray, tmin, hit ? best : tmax, tq, nprim)) {
-            hit = true;
-            best = tq;
-            best_prim = po.a;
+        Hit h;
+        bool hit;
+        if constexpr ((F & F_WORLD) != 0) {
+          // list world: the tree's winner, then the constant media that follow every tree entry in
+          // the list, in list order with the closest hit so far (their RNG draws depend on it);
+          // anything uncertain -- near ties, a chain the reference may reject, a ray that could
+          // make an inert medium draw -- runs the reference's sequential list exactly
+          constexpr int FM = F & ~(F_WORLD | F_STEP | F_BVH);  // media boundaries are primitives
+          int wobj = -1, wprim = -1;
+          int st = world_settle<F>(S, ray, tmin, overflow, bhi, second, best, best_prim, best_rank, wobj, wprim, nnode);
+          if (S.w_inert && !ray_sane(ray)) st = 2;
+          const bool exact = st == 2;
+          if constexpr ((F & F_STATS) != 0) nfall += exact ? 1u : 0u;
+          hit = st == 1;
+          // exact: every entry in list order (the reference's visit sets); else the media after the tree
+          for (int w = exact ? 0 : S.w_media; w < S.n_world; ++w) {
+            const int oi = S.world[w];
+            const rt_object o = S.objects[oi];
+            float tq;
+            int pq;
+            bool hq;
+            const float tcl = hit ? best : tmax;
+            if (o.kind == RT_OBJ_MEDIUM) {
+              hq = object_query<FM>(S, oi, ray, tmin, tcl, tq, pq, loc, nnode, nprim, nfall);
+            } else {
+              Ray rr = ray;
+              int xi = oi;
+              if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {
+                Ray moved;
+                rr = xform_ray(o, ray, moved);
+                xi = o.a;
+              }
+              const rt_object x = S.objects[xi];
+              if ((F & F_BVH) != 0 && x.kind == RT_OBJ_BVH) {
+                hq = bvh_exact<F>(S, x.a, x.b, rr, mk(1.0f / rr.d.x, 1.0f / rr.d.y, 1.0f / rr.d.z), tmin, tcl, tq, pq,
+                                  nnode, nprim, nfall);
+              } else {
+                pq = x.a;
+                hq = prim_t<F>(S, x.a, rr, tmin, tcl, tq, nprim);
+              }
+            }
+            if (hq) {
+              hit = true;
+              best = tq;
+              wobj = oi;
+              wprim = pq;
+            }
           }
+          if (hit) object_record<FM>(S, wobj, wprim, ray, tmin, best, h);
+        } else {
+          hit = bvh_settle<F>(S, obj.a, obj.b, ray, tmin, tmax, overflow, bhi, second, best, best_prim, best_rank,
+                              nnode, nprim, nfall);
+          // primitive objects after the BVH in the world list (C4's ground sphere): hittable_list's
+          // rule, t_max = the closest hit so far (inclusive), so a later entry wins a tie
+          for (int w = 1; w < S.n_world; ++w) {
+            const rt_object po = S.objects[S.world[w]];
+            float tq;
+            if (prim_t<F>(S, po.a, ray, tmin, hit ? best : tmax, tq, nprim)) {
+              hit = true;
+              best = tq;
+              best_prim = po.a;
+            }
+          }
+          if (hit) finalize<F>(S, best_prim, ray, tmin, best, h);
         }
         if (!hit) {
           contrib = att * ld3(S.bg);
           ended = true;
         } else {
-          Hit h;
-          finalize<F>(S, best_prim, ray, tmin, best, h);
           V a, em;
           RT_STAMP(6);
           if (scatter<F>(S, ray, h, a, em, loc)) {
@@ -1895,7 +2131,7 @@ void render_step_kernel(const RenderParams P) {
       if (item >= 0 && mode == 0) {
         // camera ray: its tile's candidate list (count + first entries) is loaded before the ray is
         // generated, so the loads overlap the camera arithmetic
-        const bool listed = depth == 0 && P.tile_cnt != nullptr;
+        const bool listed = (F & F_WORLD) == 0 && depth == 0 && P.tile_cnt != nullptr;
         const int32_t* ent = nullptr;
         int tcnt = -1;
         int4 g0 = make_int4(0, 0, 0, 0);
@@ -1952,10 +2188,12 @@ void render_step_kernel(const RenderParams P) {
         sp = 0;
         overflow = false;
         mode = 1;
-        if (listed && tcnt >= 0) {  // camera ray: the tile's candidate list instead of the tree
-          tile_candidates<F>(S, ent, tcnt, g0, ray, qa, rcpa, tmin, tmax, best, bhi, second, best_prim, best_rank,
-                             nprim);
-          mode = 2;
+        if constexpr ((F & F_WORLD) == 0) {
+          if (listed && tcnt >= 0) {  // camera ray: the tile's candidate list instead of the tree
+            tile_candidates<F>(S, ent, tcnt, g0, ray, qa, rcpa, tmin, tmax, best, bhi, second, best_prim, best_rank,
+                               nprim);
+            mode = 2;
+          }
         }
       }
       if (pass + 1 >= kShadePasses || __ballot(mode == 2) == 0) break;
@@ -2414,6 +2652,7 @@ struct rt_ctx {
   int features = 0;
   bool world_bvh = false;  // the world list is one BVH object (camera tile lists apply)
   bool world_step = false;  // one BVH object followed by primitive objects (render_step_kernel applies)
+  bool world_tree = false;  // a list world flattened into the world tree (render_step_kernel<..|F_WORLD>)
   int dev_nodes = 0, dev_prims = 0, dev_mats = 0, dev_texs = 0;  // device array sizes (for LDS staging)
   float last_ms = 0.0f;
   int last_sched = 0;  // RT_SCHED_* of the last render launch
@@ -2452,6 +2691,9 @@ const Variant kVariants[] = {
     RT_VARIANT_STEP(F_SPHERES | F_LDS | F_STEP),
     RT_VARIANT_STEP(F_SPHERES | F_STEP),
     RT_VARIANT_STEP(F_MESH | F_STEP),
+    RT_VARIANT_STEP(F_MESH | F_STEP | F_QLDS),
+    RT_VARIANT_STEP(F_CORNELL | F_WORLD | F_STEP),
+    RT_VARIANT_STEP(F_FINAL | F_WORLD | F_STEP),
     RT_VARIANT(F_SPHERES),
     RT_VARIANT(F_ALL),
     RT_VARIANT(F_SPHERES | F_STATS),
@@ -2480,8 +2722,9 @@ static_assert(kNumVariants <= 32, "rt_ctx::blocks_per_cu holds 32 variants");
 constexpr int kLdsBudget = 156 * 1024;  // bytes of staged nodes + primitives + stacks per workgroup
 
 // Smallest compiled variant that covers the scene's features and the requested mode.
-int pick_variant(int features, bool stats, bool exact, bool check, bool lds, bool widest = false, bool step = false) {
-  const int modes = F_STATS | F_EXACT | F_CHECK | F_LDS | F_STEP;
+int pick_variant(int features, bool stats, bool exact, bool check, bool lds, bool widest = false, bool step = false,
+                 bool world = false, bool qlds = false) {
+  const int modes = F_STATS | F_EXACT | F_CHECK | F_LDS | F_STEP | F_WORLD | F_QLDS;
   const int mode = check ? F_CHECK : ((stats ? F_STATS : 0) | (exact ? F_EXACT : 0));
   auto best_of = [&](int want) {  // covering variant with the fewest (widest: most) feature bits
     int best = -1;
@@ -2500,12 +2743,18 @@ int pick_variant(int features, bool stats, bool exact, bool check, bool lds, boo
         v = w;
         break;
       }
-  if (v >= 0 && step && mode == 0)  // its stepwise twin (world = one BVH object)
+  if (v >= 0 && step && mode == 0) {  // its stepwise twin (world = one BVH object, or the world tree)
+    int sv = -1;
     for (int w = 0; w < kNumVariants; ++w)
-      if (kVariants[w].mask == (kVariants[v].mask | F_STEP)) return w;
+      if (kVariants[w].mask == (kVariants[v].mask | F_STEP | (world ? F_WORLD : 0))) sv = w;
+    if (sv >= 0 && qlds)  // ... with its traversal tree quantized in LDS
+      for (int w = 0; w < kNumVariants; ++w)
+        if (kVariants[w].mask == (kVariants[sv].mask | F_QLDS)) return w;
+    if (sv >= 0) return sv;
+  }
   return v;
 }
-int variant_block(int v) { return (kVariants[v].mask & F_LDS) != 0 ? 1024 : 256; }
+int variant_block(int v) { return (kVariants[v].mask & (F_LDS | F_QLDS)) != 0 ? 1024 : 256; }
 
 int scene_features(const rt_scene_soa* s) {
   int f = 0;
@@ -2929,7 +3178,7 @@ int rt_ctx_create(int hip_device, rt_ctx** out) {
     c->cus = prop.multiProcessorCount;
     for (int v = 0; v < kNumVariants; ++v)
       chk(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->blocks_per_cu[v], kVariants[v].fn, variant_block(v),
-                                                       (kVariants[v].mask & F_LDS) ? kLdsBudget
+                                                       (kVariants[v].mask & (F_LDS | F_QLDS)) ? kLdsBudget
                                                                                    : variant_block(v) * (kStackDepth + locker_words(kVariants[v].mask)) * 4),
           "occupancy");
   }
@@ -3003,6 +3252,29 @@ rth::Box geom_box(const rt_prim& q, const rt_triangle* tris, float t0, float t1)
   }
   return b;
 }
+// World-space box of a child-frame box cb under instance o (translate(rotate_y(child))).
+rth::Box xform_box(const rt_object& o, const rth::Box& cb) {
+  // world = R^-1 (object) + offset, R^-1: x = c x' + s z', z = -s x' + c z' (hittable.h:112-143)
+  const double sn = (o.b & 2) ? o.f[3] : 0.0, cs = (o.b & 2) ? o.f[4] : 1.0;
+  const double off[3] = {(o.b & 1) ? o.f[0] : 0.0, (o.b & 1) ? o.f[1] : 0.0, (o.b & 1) ? o.f[2] : 0.0};
+  double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+  for (int q = 0; q < 8; ++q) {
+    const double x = (q & 1) ? cb.hi[0] : cb.lo[0], y = (q & 2) ? cb.hi[1] : cb.lo[1], z = (q & 4) ? cb.hi[2] : cb.lo[2];
+    const double w[3] = {cs * x + sn * z + off[0], y + off[1], -sn * x + cs * z + off[2]};
+    for (int k = 0; k < 3; ++k) {
+      lo[k] = std::min(lo[k], w[k]);
+      hi[k] = std::max(hi[k], w[k]);
+    }
+  }
+  rth::Box out;
+  for (int k = 0; k < 3; ++k) {  // widened for the float rounding of the instance transform
+    const double pad = 1e-5 * (std::fabs(lo[k]) + std::fabs(hi[k]) + (hi[k] - lo[k])) + 1e-6;
+    out.lo[k] = (float)(lo[k] - pad);
+    out.hi[k] = (float)(hi[k] + pad);
+  }
+  return out;
+}
+
 // World-space box over the shutter [t0, t1] of object oi (an instance's child box through its
 // rotate_y + translate, a medium's boundary); false when it cannot be bounded.
 bool object_box(const rt_scene_soa* s, int oi, float t0, float t1, rth::Box& out, int depth = 0) {
@@ -3035,27 +3307,196 @@ bool object_box(const rt_scene_soa* s, int oi, float t0, float t1, rth::Box& out
     case RT_OBJ_XFORM: {
       rth::Box cb;
       if (!object_box(s, o.a, t0, t1, cb, depth + 1)) return false;
-      // world = R^-1 (object) + offset, R^-1: x = c x' + s z', z = -s x' + c z' (hittable.h:112-143)
-      const double sn = (o.b & 2) ? o.f[3] : 0.0, cs = (o.b & 2) ? o.f[4] : 1.0;
-      const double off[3] = {(o.b & 1) ? o.f[0] : 0.0, (o.b & 1) ? o.f[1] : 0.0, (o.b & 1) ? o.f[2] : 0.0};
-      double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
-      for (int q = 0; q < 8; ++q) {
-        const double x = (q & 1) ? cb.hi[0] : cb.lo[0], y = (q & 2) ? cb.hi[1] : cb.lo[1], z = (q & 4) ? cb.hi[2] : cb.lo[2];
-        const double w[3] = {cs * x + sn * z + off[0], y + off[1], -sn * x + cs * z + off[2]};
-        for (int k = 0; k < 3; ++k) {
-          lo[k] = std::min(lo[k], w[k]);
-          hi[k] = std::max(hi[k], w[k]);
-        }
-      }
-      for (int k = 0; k < 3; ++k) {  // widened for the float rounding of the instance transform
-        const double pad = 1e-5 * (std::fabs(lo[k]) + std::fabs(hi[k]) + (hi[k] - lo[k])) + 1e-6;
-        out.lo[k] = (float)(lo[k] - pad);
-        out.hi[k] = (float)(hi[k] + pad);
-      }
+      out = xform_box(o, cb);
       return true;
     }
   }
   return false;
+}
+
+// World tree (F_WORLD): a list world (hittable_list.h:23-39) of primitives, BVHs and translate /
+// rotate_y instances of them, followed by constant media, flattened into ONE traversal tree over
+// every primitive of every non-medium entry (world-space boxes over the shutter; an instance's
+// primitives through its transform, padded), so the whole world query is one candidate search in
+// render_step_kernel instead of a loop over entries with a traversal per BVH.  Each leaf keeps its
+// entry's semantics: it is tested in its instance's frame, its tie key orders exact ties as the list
+// does (a later entry wins) and, inside a BVH entry, as bvh.h does (the lower reference leaf rank
+// wins), and a BVH member's winner is validated on that BVH's reference chain (world_settle).
+// Media must follow every tree entry in the list (they draw from the RNG with the closest hit so far
+// as their t_max), except inert ones: a medium bounded by a sphere never reaches its draw (H1: the
+// second boundary query returns nothing or t1 itself) unless its boundary root is NaN, which a
+// sane ray (ray_sane) cannot produce.  Leaves: 4 float4 each (see DScene::wleaf).
+static bool build_world_tree(const rt_scene_soa* s, const std::vector<rt_prim>& prims, std::vector<rt_bvh_node>& nodes,
+                             std::vector<float4>& wleaf, std::vector<float4>& wxf, int& wt_fb, int& w_media,
+                             int& w_inert) {
+  const int NW = s->n_world;
+  if (NW < 2 || NW >= (1 << (31 - RT_WKEY_SHIFT))) return false;
+  auto obj = [&](int k) -> const rt_object& { return s->objects[k]; };
+  int last_tree = -1;
+  for (int w = 0; w < NW; ++w)
+    if (obj(s->world[w]).kind != RT_OBJ_MEDIUM) last_tree = w;
+  if (last_tree < 0) return false;
+  w_inert = 0;
+  for (int w = 0; w < NW; ++w) {
+    const rt_object& o = obj(s->world[w]);
+    if (o.kind == RT_OBJ_MEDIUM) {
+      const rt_object& bo = obj(o.a);
+      if (w < last_tree) {  // must be inert: a bounded static sphere, or a moving one with t1 > t0
+        if (bo.kind != RT_OBJ_PRIM) return false;
+        const rt_prim& q = s->prims[bo.a];
+        const int ty = q.type & 0xff;
+        if (ty != RT_PRIM_SPHERE && ty != RT_PRIM_MOVING_SPHERE) return false;
+        const int np = ty == RT_PRIM_SPHERE ? 4 : 9;
+        for (int k = 0; k < np; ++k)
+          if (!(std::fabs(q.p[k]) < 1e6f)) return false;
+        if (ty == RT_PRIM_MOVING_SPHERE && !(q.p[8] != 0.0f)) return false;
+        w_inert = 1;
+      } else if (!(bo.kind == RT_OBJ_PRIM || (bo.kind == RT_OBJ_XFORM && obj(bo.a).kind == RT_OBJ_PRIM))) {
+        return false;  // active media: primitive boundaries (object_query's direct path)
+      }
+    } else if (o.kind == RT_OBJ_XFORM) {
+      const int ck = obj(o.a).kind;
+      if (ck != RT_OBJ_PRIM && ck != RT_OBJ_BVH) return false;
+    } else if (o.kind != RT_OBJ_PRIM && o.kind != RT_OBJ_BVH) {
+      return false;
+    }
+  }
+  w_media = last_tree + 1;
+  struct Leaf {
+    int prim, xf, w, bobj, rank;
+  };
+  std::vector<Leaf> leaves;
+  std::vector<rth::Box> box;
+  std::vector<int> xf_of(s->n_objects, -1);
+  const float t0 = std::fmin(s->camera.time0, s->camera.time1), t1 = std::fmax(s->camera.time0, s->camera.time1);
+  for (int w = 0; w < w_media; ++w) {
+    int oi = s->world[w];
+    if (obj(oi).kind == RT_OBJ_MEDIUM) continue;  // inert
+    int xf = -1, xo = -1;
+    if (obj(oi).kind == RT_OBJ_XFORM) {
+      xo = oi;
+      if (xf_of[oi] < 0) {
+        const rt_object& o = obj(oi);
+        int32_t bits = o.b;
+        float fb;
+        memcpy(&fb, &bits, 4);
+        xf_of[oi] = (int)wxf.size() / 2;
+        wxf.push_back(make_float4(o.f[0], o.f[1], o.f[2], fb));
+        wxf.push_back(make_float4(o.f[3], o.f[4], 0.0f, 0.0f));
+      }
+      xf = xf_of[oi];
+      oi = obj(oi).a;
+    }
+    auto add = [&](int pid, int bobj, int rank) {
+      rth::Box b = geom_box(s->prims[pid], s->triangles, t0, t1);
+      if (xo >= 0) b = xform_box(obj(xo), b);
+      leaves.push_back(Leaf{pid, xf, w, bobj, rank});
+      box.push_back(b);
+    };
+    const rt_object& o = obj(oi);
+    if (o.kind == RT_OBJ_PRIM) {
+      add(o.a, -1, 0);
+    } else {  // BVH: its reference leaves, with their ranks in the reference's depth-first order
+      if (o.b > RT_WKEY_SHIFT) return false;
+      const int inner = (1 << o.b) - 1, last0 = (1 << (o.b - 1)) - 1;
+      for (int k = last0; k < inner; ++k) {
+        const int ids[2] = {s->nodes[o.a + k].leaf_a, s->nodes[o.a + k].leaf_b};
+        for (int q = 0; q < 2; ++q)
+          if (ids[q] >= 0) add(ids[q], oi, 2 * (k - last0) + q);
+      }
+    }
+  }
+  const int n = (int)leaves.size();
+  if (n < 2 || n >= (1 << 24)) return false;
+  wleaf.resize(4 * (size_t)n);
+  for (int i = 0; i < n; ++i) {
+    const Leaf& L = leaves[(size_t)i];
+    rt_prim q = prims[(size_t)L.prim];  // the device record: flags, triangle operands
+    const int32_t key = ((NW - 1 - L.w) << RT_WKEY_SHIFT) | L.rank;
+    memcpy(&q.p[9], &key, 4);
+    if (L.xf >= 0) q.type |= RT_PRIM_FLAG_XF;
+    memcpy(&wleaf[4 * (size_t)i], &q, sizeof(q));
+    const int32_t d[4] = {L.xf, L.w, L.bobj, L.prim};
+    memcpy(&wleaf[4 * (size_t)i + 3], d, sizeof(d));
+  }
+  std::vector<int> ids(n);
+  for (int i = 0; i < n; ++i) ids[(size_t)i] = i;
+  wt_fb = (int)nodes.size();
+  nodes.resize(wt_fb + 2);  // record 0 = root
+  SahBuilder sb{box, nodes, wt_fb};
+  sb.build(ids.data(), n, 0);
+  return true;
+}
+
+// Quantized traversal tree (F_QLDS; qpair): the world BVH's traversal-tree pair records, `npairs` of
+// them from rt_bvh_node index fb, as 24-byte records that fit LDS next to 16-bit stacks (C4's door:
+// 4 329 pairs = 104 KB + 32 KB of stacks, instead of 277 KB in L2).  Per pair and axis: an origin
+// rounded down to binary16 below both children, a power-of-two scale 2^E with 255 * 2^E covering the
+// pair's extent, and each child's padded box as bytes rounded outward.  False when a value does
+// not fit (binary16 range, scales spread over more than 32 octaves, child words beyond 16 bits).
+static bool build_qtree(const std::vector<rt_bvh_node>& nodes, int fb, int npairs, std::vector<uint32_t>& out,
+                        int& ebias) {
+  auto half_down = [](double x, uint16_t& bits) {
+    if (!(std::fabs(x) < 60000.0)) return false;
+    _Float16 h = (_Float16)(float)x;
+    memcpy(&bits, &h, 2);
+    while ((double)(float)h > x) {  // step down one binary16 ulp
+      bits = (bits & 0x8000u) ? (uint16_t)(bits + 1) : (bits == 0 ? (uint16_t)0x8001u : (uint16_t)(bits - 1));
+      memcpy(&h, &bits, 2);
+    }
+    return true;
+  };
+  std::vector<int> E((size_t)npairs * 3);
+  std::vector<uint16_t> org((size_t)npairs * 3);
+  int emax = -1000;
+  for (int i = 0; i < npairs; ++i) {
+    const rt_bvh_node* r = &nodes[(size_t)fb + 2 * (size_t)i];
+    for (int a = 0; a < 3; ++a) {
+      const double mn = std::min(r[0].lo[a], r[1].lo[a]), mx = std::max(r[0].hi[a], r[1].hi[a]);
+      uint16_t ob;
+      if (!half_down(mn, ob) || !(mx >= mn) || !(mx < 60000.0)) return false;
+      _Float16 h;
+      memcpy(&h, &ob, 2);
+      const double ext = mx - (double)(float)h;
+      int e = -60;
+      while (255.0 * std::ldexp(1.0, e) < ext) ++e;
+      org[3 * (size_t)i + a] = ob;
+      E[3 * (size_t)i + a] = e;
+      emax = std::max(emax, e);
+    }
+  }
+  ebias = emax - 31;  // a scale below 2^ebias is widened to it: coarser, still covering
+  if (ebias < -120 || emax > 100) return false;
+  out.assign((size_t)npairs * 6, 0u);
+  for (int i = 0; i < npairs; ++i) {
+    const rt_bvh_node* r = &nodes[(size_t)fb + 2 * (size_t)i];
+    uint32_t ee = 0;
+    uint8_t q[2][6];
+    for (int a = 0; a < 3; ++a) {
+      const int e = std::max(E[3 * (size_t)i + a], ebias);
+      ee |= (uint32_t)(e - ebias) << (5 * a);
+      _Float16 h;
+      memcpy(&h, &org[3 * (size_t)i + a], 2);
+      const double o = (double)(float)h, sc = std::ldexp(1.0, e);
+      for (int ch = 0; ch < 2; ++ch) {
+        const double lo = std::floor(((double)r[ch].lo[a] - o) / sc), hi = std::ceil(((double)r[ch].hi[a] - o) / sc);
+        if (!(lo >= 0.0 && hi <= 255.0 && lo <= hi)) return false;
+        if (!(o + lo * sc <= (double)r[ch].lo[a] && o + hi * sc >= (double)r[ch].hi[a])) return false;
+        q[ch][a] = (uint8_t)lo;
+        q[ch][3 + a] = (uint8_t)hi;
+      }
+    }
+    const int c0 = r[0].leaf_a, c1 = r[0].leaf_b;
+    if (c0 < -32768 || c0 > 32767 || c1 < -32768 || c1 > 32767) return false;
+    uint32_t* w = &out[6 * (size_t)i];
+    w[0] = (uint32_t)org[3 * (size_t)i] | (uint32_t)org[3 * (size_t)i + 1] << 16;
+    w[1] = (uint32_t)org[3 * (size_t)i + 2] | ee << 16;
+    const uint8_t b[12] = {q[0][0], q[0][1], q[0][2], q[0][3], q[0][4], q[0][5],
+                           q[1][0], q[1][1], q[1][2], q[1][3], q[1][4], q[1][5]};
+    memcpy(&w[2], b, 12);
+    w[5] = ((uint32_t)c0 & 0xffffu) | ((uint32_t)c1 << 16);
+  }
+  return true;
 }
 
 int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
@@ -3115,6 +3556,23 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
     }
     p.type |= ti << 12;
   }
+  bool world_step = s->n_world <= 8 && s->objects[s->world[0]].kind == RT_OBJ_BVH;
+  for (int w = 1; w < s->n_world; ++w) world_step = world_step && s->objects[s->world[w]].kind == RT_OBJ_PRIM;
+  std::vector<float4> wleaf, wxf;
+  int wt_fb = -1, w_media = 0, w_inert = 0;
+  const bool world_tree = !world_step && !getenv("RT_NO_WORLD_TREE") &&  // (env: A/B experiments)
+                          build_world_tree(s, prims, nodes, wleaf, wxf, wt_fb, w_media, w_inert);
+  std::vector<uint32_t> qnodes;
+  int q_pairs = 0, q_ebias = 0;
+  if (world_step && !getenv("RT_NO_QLDS")) {  // the world BVH's traversal tree, quantized (F_QLDS)
+    const rt_object& wo = objects[(size_t)s->world[0]];
+    int n = 0;
+    const int inner = (1 << wo.b) - 1, last0 = (1 << (wo.b - 1)) - 1;
+    for (int k = last0; k < inner; ++k) n += (s->nodes[wo.a + k].leaf_a >= 0) + (s->nodes[wo.a + k].leaf_b >= 0);
+    if (n >= 2 && (size_t)(n - 1) * 24 + 1024 * kStackDepth * 2 <= (size_t)kLdsBudget &&
+        build_qtree(nodes, wo.c, n - 1, qnodes, q_ebias))
+      q_pairs = n - 1;
+  }
   DScene& d = c->scene;
   d = DScene{};
   const rt_prim* dp;
@@ -3133,6 +3591,14 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   if ((rc = upload(c, s->perlins, (size_t)s->n_perlins, &d.perlins))) return rc;
   if ((rc = upload(c, s->images, (size_t)s->n_images, &d.images))) return rc;
   if ((rc = upload(c, s->texels, (size_t)s->n_texels, &d.texels))) return rc;
+  if ((rc = upload(c, wleaf.data(), wleaf.size(), &d.wleaf))) return rc;
+  if ((rc = upload(c, wxf.data(), wxf.size(), &d.wxf))) return rc;
+  d.wt_fb = wt_fb;
+  d.w_media = w_media;
+  d.w_inert = w_inert;
+  if (q_pairs > 0 && (rc = upload(c, qnodes.data(), qnodes.size(), &d.qnodes))) return rc;
+  d.q_pairs = q_pairs;
+  d.q_ebias = q_ebias;
   d.prims = (const float4*)dp;
   d.nodes = (const float4*)dn;
   d.mats = (const int4*)dm;
@@ -3143,8 +3609,8 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   d.bg[2] = s->background[2];
   c->features = scene_features(s);
   c->world_bvh = s->n_world == 1 && s->objects[s->world[0]].kind == RT_OBJ_BVH;
-  c->world_step = s->n_world <= 8 && s->objects[s->world[0]].kind == RT_OBJ_BVH;
-  for (int w = 1; w < s->n_world; ++w) c->world_step = c->world_step && s->objects[s->world[w]].kind == RT_OBJ_PRIM;
+  c->world_step = world_step;
+  c->world_tree = world_tree;
   c->bin_sph = nullptr;
   c->bin_ids = nullptr;
   c->bin_n = 0;
@@ -3362,9 +3828,10 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
       (size_t)(2 * c->dev_nodes + 3 * c->dev_prims + (c->dev_prims + 1) / 2 + c->dev_mats + 2 * c->dev_texs) * sizeof(float4);
   const bool use_lds = lds_bytes + 1024 * kStackDepth * 2 <= (size_t)kLdsBudget && c->dev_nodes / 2 < 32768 &&
                        c->dev_prims < 32768 && (a->flags & RT_FLAG_NO_LDS) == 0;
-  const bool step = c->world_step && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
+  const bool step = (c->world_step || c->world_tree) && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
+  const bool qlds = !use_lds && c->scene.q_pairs > 0 && (a->flags & RT_FLAG_NO_LDS) == 0;
   const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
-                               (a->flags & RT_FLAG_WIDEST) != 0, step);
+                               (a->flags & RT_FLAG_WIDEST) != 0, step, c->world_tree, qlds);
   if (var < 0) return fail(c, RT_ERR_SCENE, "no kernel variant covers the scene features");
   // shading phase of render_step_kernel once this many lanes of a wave wait (RT_SHADE_MIN: tuning)
   // (measured: C2 best at 60 of 64 lanes; C4's triangle-mesh steps at 48: 125.0 -> 119.7 ms, 40: 121.8)
@@ -3477,7 +3944,10 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   P.S.lds_prims = lds_var ? c->dev_prims : 0;
   P.S.lds_mats = lds_var ? c->dev_mats : 0;
   P.S.lds_texs = lds_var ? c->dev_texs : 0;
-  const size_t shmem = lds_var ? lds_bytes + (size_t)bs * kStackDepth * 2 : (size_t)bs * (kStackDepth + locker_words(kVariants[var].mask)) * 4;
+  const bool qlds_var = (kVariants[var].mask & F_QLDS) != 0;
+  const size_t shmem = lds_var    ? lds_bytes + (size_t)bs * kStackDepth * 2
+                       : qlds_var ? (size_t)c->scene.q_pairs * 24 + (size_t)bs * kStackDepth * 2
+                                  : (size_t)bs * (kStackDepth + locker_words(kVariants[var].mask)) * 4;
   // Camera-ray culling, built once per (scene, W, H): candidate lists for the stepwise kernel
   // (world = one BVH), top-level entry masks for list worlds.  Not in the exact / audit modes,
   // whose counters are the reference's.
