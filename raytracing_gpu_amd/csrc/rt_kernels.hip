@@ -175,7 +175,8 @@ constexpr int kStackDepth = 16;
 // lane-interleaved (word k of thread t at [k * block + t]), instead of VGPRs: it is touched once
 // per sample, and without it the variants' live state spills to scratch inside the traversal
 // loops (F_FINAL: 744 B per lane, ~340 B of scratch stores per segment, missing L2).
-constexpr int kLocker = 21;  // words 15..20: the lane's RNG state, lane-contiguous (6 words per lane)
+constexpr int kLocker = 23;  // words 15..20: the lane's RNG state, lane-contiguous (6 words per lane);
+                             // 21, 22: split-sample end and claim (s_end, ck)
 constexpr int kLockerSmall = 5;  // variants that park only the sample sum, fb and row
 // Variants that also park the per-segment state (locker words 5..20: column, row, sample, depth,
 // counts, attenuation, RNG state): the widest global-memory variants, whose world query spills to
@@ -185,9 +186,13 @@ constexpr int kLockerSmall = 5;  // variants that park only the sample sum, fb a
 constexpr bool parks_segment_mask(int mask) {
   return (mask & (F_LDS | F_STEP)) == 0 && ((mask & F_ALL) == F_FINAL || (mask & F_ALL) == F_ALL);
 }
-// (render_step_kernel keeps no locker: only its traversal stack is in LDS)
+// render_step_kernel: the world-tree variants park their per-item / per-sample state in a locker
+// of kLockerStep words (step_parks_mask); the others keep none (only the traversal stack is in LDS).
+constexpr int kLockerStep = 24;  // 18 state words + the RNG state (6 words, lane-contiguous)
+constexpr bool step_parks_mask(int mask) { return (mask & F_STEP) != 0 && (mask & F_WORLD) != 0; }
 constexpr int locker_words(int mask) {
-  return (mask & F_STEP) != 0 ? 0 : (parks_segment_mask(mask) ? kLocker : kLockerSmall);
+  return (mask & F_STEP) != 0 ? (step_parks_mask(mask) ? kLockerStep : 0)
+                              : (parks_segment_mask(mask) ? kLocker : kLockerSmall);
 }
 // Word k of the locker as a T lvalue for parking variants, else the register copy `reg`.
 template <bool PK, typename T>
@@ -1696,6 +1701,10 @@ void render_kernel(const RenderParams P) {
   unsigned& item_segs = cold_ref<PK>(item_segs_r, lk + 9 * LB);
   unsigned& nseg = cold_ref<PK>(nseg_r, lk + 10 * LB);
   unsigned& nsamp = cold_ref<PK>(nsamp_r, lk + 11 * LB);
+  // split samples (see render_step_kernel): the item ends after sample s_end - 1; ck = the split claim
+  int s_end_r = 0, ck_r = -1;
+  int& s_end = cold_ref<PK>(s_end_r, lk + 21 * LB);
+  int& ck = cold_ref<PK>(ck_r, lk + 22 * LB);
   if constexpr (PK) {
     nseg = 0;
     nsamp = 0;
@@ -1740,7 +1749,23 @@ void render_kernel(const RenderParams P) {
         if (mine >= P.total_items) {
           done = true;
         } else {
-          item = P.perm ? (long long)P.perm[mine] : (long long)mine;
+          unsigned long long pos = mine;
+          int sa = 0;
+          ck = -1;
+          if (P.split_mode == 2) {  // split samples and the other items, claimed in one sequence
+            const unsigned long long nsub = P.n_split * (unsigned long long)P.spp;
+            const unsigned long long v = P.order ? (unsigned long long)P.order[mine] : mine;
+            if (v < nsub) {
+              pos = v / (unsigned)P.spp;
+              sa = (int)(v - pos * (unsigned)P.spp);
+              ck = (int)v;
+            } else {
+              pos = v - nsub + P.n_split;
+            }
+          } else if (P.split_mode == 1 && mine < P.n_split) {
+            ck = (int)mine;
+          }
+          item = P.perm ? (long long)P.perm[pos] : (long long)pos;
           // Row-major, fb inside the row, rows in row_order: the costliest rows of the previous
           // launch of this configuration first (else bottom to top), so a launch does not end
           // with a long item started late (a lane runs an item's samples serially).
@@ -1754,9 +1779,11 @@ void render_kernel(const RenderParams P) {
           const long long id = P.fb_first + f;
           const long long p = (long long)j * P.W + i;
           const long long slot = ((id + 1) * p + id + 1) % P.npix;  // render.h:101 (H3)
-          const uint4 s0 = P.states[2 * slot], s1 = P.states[2 * slot + 1];
+          const uint4* st = sa > 0 ? P.ckpt + 2 * (long long)ck : P.states + 2 * slot;
+          const uint4 s0 = st[0], s1 = st[1];
           loc.d = s0.x; loc.v[0] = s0.y; loc.v[1] = s0.z; loc.v[2] = s0.w; loc.v[3] = s1.x; loc.v[4] = s1.y;
-          s = 0;
+          s = sa;
+          s_end = (P.split_mode == 2 && ck >= 0) ? sa + 1 : P.spp;
           depth = 0;
           item_segs = 0;
           if constexpr (parks<F>()) {
@@ -1776,6 +1803,11 @@ void render_kernel(const RenderParams P) {
       // ---- begin a sample: jitter + camera ray (render.h:105-108, camera.h:49-58)
       if (depth == 0) {
         RT_STAMP(1);
+        if (P.split_mode == 1 && ck >= 0 && s > 0) {  // record the sample-start state for split launches
+          uint4* dst = P.ckpt + 2 * ((long long)ck * P.spp + s);
+          dst[0] = make_uint4(loc.d, loc.v[0], loc.v[1], loc.v[2]);
+          dst[1] = make_uint4(loc.v[3], loc.v[4], item_segs, 0u);
+        }
         {
           Rng lr = loc;
           camera_ray(P, C, i, j, s, per_pixel, lr, ray);
@@ -1841,16 +1873,24 @@ void render_kernel(const RenderParams P) {
         }
         depth = 0;
         ++nsamp;
-        if (++s == P.spp) {
-          const V out = (1.0f / (float)P.spp) * col;
-          if constexpr (parks<F>()) {
-            f = (int)lk[3 * LB];
-            r = (int)lk[4 * LB];
+        if (++s == s_end) {
+          if (P.split_mode == 2 && ck >= 0) {  // one sample of a split item: its sum, merged later
+            float* dst = P.contrib + 3 * (long long)ck;
+            dst[0] = col.x;
+            dst[1] = col.y;
+            dst[2] = col.z;
+          } else {
+            const V out = (1.0f / (float)P.spp) * col;
+            if constexpr (parks<F>()) {
+              f = (int)lk[3 * LB];
+              r = (int)lk[4 * LB];
+            }
+            float* dst = P.fb + 3 * (((long long)f * P.rows + r) * P.W + i);
+            dst[0] = out.x;
+            dst[1] = out.y;
+            dst[2] = out.z;
           }
-          float* dst = P.fb + 3 * (((long long)f * P.rows + r) * P.W + i);
-          dst[0] = out.x;
-          dst[1] = out.y;
-          dst[2] = out.z;
+          if (P.split_mode == 1 && ck >= 0) P.ckpt[2 * (long long)ck * P.spp + 1] = make_uint4(0u, 0u, item_segs, 0u);
           if (P.row_cost && (i & 15) == 0) atomicAdd(&P.row_cost[j], (unsigned long long)item_segs);  // a sample ranks rows
           if (P.item_cost) P.item_cost[item] = (uint16_t)(item_segs < 65535u ? item_segs : 65535u);
           item = -1;
@@ -1922,24 +1962,63 @@ void render_step_kernel(const RenderParams P) {
   long long item = -1;  // -1: no item
   bool done = false;
   int mode = 0;  // 0: between queries, 1: traversing, 2: search ended, shading pending
-  int f = 0, i = 0, r = 0, j = 0, s = 0, depth = 0;
-  Rng loc{}, cam{};
+  // Per-item / per-sample state, touched only between queries.  The world-tree variants (PKS) keep it
+  // in an LDS locker after the stacks (word k of thread t at [k * block + t]; the RNG state
+  // lane-contiguous after them) instead of VGPRs, which the traversal loop needs (C5: the variant
+  // needs ~190 VGPRs otherwise, far above the 128 of 4 waves/SIMD); their REF camera offsets come
+  // from cam_tab, as in render_kernel, instead of a camera RNG copy.
+  constexpr bool PKS = step_parks_mask(F);
+  constexpr int LB = render_block<F>();
+  uint32_t* const lk = (uint32_t*)rt_lds + LB * kStackDepth + threadIdx.x;
+  int f_r = 0, i_r = 0, r_r = 0, j_r = 0, s_r = 0, depth_r = 0, ck_r = -1, lng_r = 0, fresh_r = 0;
+  unsigned nseg_r = 0, nsamp_r = 0, item_segs_r = 0;
+  int& f = cold_ref<PKS>(f_r, lk + 0 * LB);
+  int& i = cold_ref<PKS>(i_r, lk + 1 * LB);
+  int& r = cold_ref<PKS>(r_r, lk + 2 * LB);
+  int& j = cold_ref<PKS>(j_r, lk + 3 * LB);
+  int& s = cold_ref<PKS>(s_r, lk + 4 * LB);
+  int& depth = cold_ref<PKS>(depth_r, lk + 5 * LB);
+  unsigned& item_segs = cold_ref<PKS>(item_segs_r, lk + 6 * LB);
+  unsigned& nseg = cold_ref<PKS>(nseg_r, lk + 7 * LB);
+  unsigned& nsamp = cold_ref<PKS>(nsamp_r, lk + 8 * LB);
+  int& ck = cold_ref<PKS>(ck_r, lk + 9 * LB);  // split_mode 1: perm position whose sample-start states are
+                                               // recorded; 2: split sample (the item ends after it)
+  int& lng = cold_ref<PKS>(lng_r, lk + 10 * LB);  // the item is one of the longest of the previous launch
+  int& fresh = cold_ref<PKS>(fresh_r, lk + 11 * LB);  // the item's first sample is next (camera state)
+  if constexpr (PKS) {
+    nseg = 0;
+    nsamp = 0;
+    ck = -1;
+    lng = 0;
+  }
+  float* const lkf = reinterpret_cast<float*>(lk);
+  V att_r = mk(1, 1, 1), col_r = mk(0, 0, 0);
+  auto vget = [&](V& reg, int w) -> V {
+    if constexpr (PKS) return mk(lkf[w * LB], lkf[(w + 1) * LB], lkf[(w + 2) * LB]);
+    else return reg;
+  };
+  auto vset = [&](V& reg, int w, V a) {
+    if constexpr (PKS) {
+      lkf[w * LB] = a.x;
+      lkf[(w + 1) * LB] = a.y;
+      lkf[(w + 2) * LB] = a.z;
+    } else {
+      reg = a;
+    }
+  };
+  Rng loc_r{}, cam{};
+  Rng& loc = cold_ref<PKS>(loc_r, (uint32_t*)rt_lds + LB * (kStackDepth + 18) + 6 * threadIdx.x);
+  int s_end_r = 0;  // the lane's item ends after sample s_end - 1 (spp, or one sample of a split item)
   Ray ray{};
-  V att = mk(1, 1, 1), col = mk(0, 0, 0);
   V finv = mk(0, 0, 0), oi = mk(0, 0, 0);
   int cur = 0, sp = 0, best_prim = -1, best_rank = 0x7fffffff;
   float best = 0.0f, bhi = 0.0f, second = 0.0f, qa = 0.0f, rcpa = 0.0f;
   bool overflow = false;
-  unsigned nseg = 0, nsamp = 0, item_segs = 0;
   unsigned nnode = 0, nprim = 0, nfall = 0;
   const bool per_pixel = P.cam_mode == RT_CAM_PER_PIXEL;
   const rt_camera& C = S.cam;
   unsigned long long chunk_base = 0;  // wave-uniform: next unclaimed item of the wave's chunk
   unsigned chunk_left = 0;
-  bool lng = false;  // the lane's item is one of the longest of the previous launch (perm prefix)
-  int s_end = 0;     // the lane's item ends after sample s_end - 1 (spp, or one sample of a split item)
-  int ck = -1;       // split_mode 1: perm position whose sample-start states are recorded; 2: split sample
-  bool fresh = false;  // the item's first sample is next (camera state from its start)
 #ifdef RT_WAVE_TIMES
   unsigned long long wt0, wt1 = 0;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wt0)::"memory");
@@ -2025,28 +2104,40 @@ void render_step_kernel(const RenderParams P) {
           if (hit) finalize<F>(S, best_prim, ray, tmin, best, h);
         }
         if (!hit) {
-          contrib = att * ld3(S.bg);
+          contrib = vget(att_r, 15) * ld3(S.bg);
           ended = true;
         } else {
           V a, em;
           RT_STAMP(6);
-          if (scatter<F>(S, ray, h, a, em, loc)) {
-            att = att * a;
+          bool sc;
+          if constexpr (PKS) {  // on a register copy of the parked state
+            Rng lr = loc;
+            sc = scatter<F>(S, ray, h, a, em, lr);
+            loc = lr;
+          } else {
+            sc = scatter<F>(S, ray, h, a, em, loc);
+          }
+          if (sc) {
+            vset(att_r, 15, vget(att_r, 15) * a);
             if (++depth == P.max_depth) {
               contrib = mk(0.0f, 0.0f, 0.0f);
               ended = true;
             }
           } else {
-            contrib = att * em;
+            contrib = vget(att_r, 15) * em;
             ended = true;
           }
         }
         RT_STAMP(0);
         if (ended) {
-          col = col + contrib;
+          const V col = vget(col_r, 12) + contrib;
+          vset(col_r, 12, col);
           depth = 0;
           ++nsamp;
-          if (++s == s_end) {
+          // the item ends after sample spp - 1, a split item's sample (split_mode 2) after itself
+          // (parking variants derive it from ck: sample ck % spp)
+          if constexpr (PKS) s_end_r = (P.split_mode == 2 && ck >= 0) ? ck - (ck / P.spp) * P.spp + 1 : P.spp;
+          if (++s == s_end_r) {
             if (P.split_mode == 2 && ck >= 0) {  // one sample of a split item: its sum, merged later
               float* dst = P.contrib + 3 * (long long)ck;
               dst[0] = col.x;
@@ -2097,7 +2188,7 @@ void render_step_kernel(const RenderParams P) {
               ck = (int)mine;
             }
             item = P.perm ? (long long)P.perm[pos] : (long long)pos;
-            lng = pos < P.n_long;
+            lng = pos < P.n_long ? 1 : 0;
             const long long per_row = (long long)P.fb_count * P.W;  // same item order as render_kernel
             const int q = (int)(item / per_row);
             const long long rem = item - (long long)q * per_row;
@@ -2112,18 +2203,18 @@ void render_step_kernel(const RenderParams P) {
             const uint4 s0 = st[0], s1 = st[1];
             loc.d = s0.x; loc.v[0] = s0.y; loc.v[1] = s0.z; loc.v[2] = s0.w; loc.v[3] = s1.x; loc.v[4] = s1.y;
             s = sa;
-            s_end = (P.split_mode == 2 && ck >= 0) ? sa + 1 : P.spp;
-            fresh = true;
+            if constexpr (!PKS) s_end_r = (P.split_mode == 2 && ck >= 0) ? sa + 1 : P.spp;
+            fresh = 1;
             depth = 0;
             item_segs = 0;
-            col = mk(0, 0, 0);
+            vset(col_r, 12, mk(0, 0, 0));
           }
         }
       }
       // Waves holding one of the longest items (processed first) issue ahead of the others, so the
       // long items of a small multi-GPU share are not the last to finish.
       if (P.n_long > 0) {
-        if (__ballot(item >= 0 && lng) != 0) __builtin_amdgcn_s_setprio(3);
+        if (__ballot(item >= 0 && lng != 0) != 0) __builtin_amdgcn_s_setprio(3);
         else __builtin_amdgcn_s_setprio(0);
       }
       // ---- next query: camera ray at a sample's start (render.h:105-108, camera.h:49-58)
@@ -2141,7 +2232,17 @@ void render_step_kernel(const RenderParams P) {
           tcnt = P.tile_cnt[t];
           g0 = *reinterpret_cast<const int4*>(ent);
         }
-        if (depth == 0) {
+        if (depth == 0 && PKS) {
+          if (P.split_mode == 1 && ck >= 0 && s > 0) {  // record the sample-start state for split launches
+            uint4* dst = P.ckpt + 2 * ((long long)ck * P.spp + s);
+            dst[0] = make_uint4(loc.d, loc.v[0], loc.v[1], loc.v[2]);
+            dst[1] = make_uint4(loc.v[3], loc.v[4], item_segs, 0u);
+          }
+          Rng lr = loc;
+          camera_ray(P, C, i, j, s, per_pixel, lr, ray);  // REF offsets from cam_tab
+          loc = lr;
+          vset(att_r, 15, mk(1.0f, 1.0f, 1.0f));
+        } else if (depth == 0) {
           // REF: the step kernel draws the per-sample lens offset and time from its own copy of the
           // pristine slot-0 state instead of cam_tab (measured faster here: the table read would sit
           // in the shading phase's dependent chain)
@@ -2154,7 +2255,7 @@ void render_step_kernel(const RenderParams P) {
               cam.d = c0.x; cam.v[0] = c0.y; cam.v[1] = c0.z; cam.v[2] = c0.w; cam.v[3] = c1.x; cam.v[4] = c1.y;
             }
           }
-          fresh = false;
+          fresh = 0;
           if (P.split_mode == 1 && ck >= 0 && s > 0) {  // record the sample-start state for split launches
             uint4* dst = P.ckpt + 2 * ((long long)ck * P.spp + s);
             dst[0] = make_uint4(loc.d, loc.v[0], loc.v[1], loc.v[2]);
@@ -2168,7 +2269,7 @@ void render_step_kernel(const RenderParams P) {
           ray.o = ld3(C.origin) + off;
           ray.d = ld3(C.lower_left) + u * ld3(C.horizontal) + v * ld3(C.vertical) - ld3(C.origin) - off;
           ray.tm = urange(cr, C.time0, C.time1);
-          att = mk(1.0f, 1.0f, 1.0f);
+          vset(att_r, 15, mk(1.0f, 1.0f, 1.0f));
         }
         // traversal reciprocals: hardware v_rcp_f32 (1 ulp; the tree's boxes are padded by 2^-16
         // relative, far above either reciprocal's rounding) instead of three IEEE divides
@@ -3560,7 +3661,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   for (int w = 1; w < s->n_world; ++w) world_step = world_step && s->objects[s->world[w]].kind == RT_OBJ_PRIM;
   std::vector<float4> wleaf, wxf;
   int wt_fb = -1, w_media = 0, w_inert = 0;
-  const bool world_tree = !world_step && !getenv("RT_NO_WORLD_TREE") &&  // (env: A/B experiments)
+  // The world tree is opt-in (RT_WORLD_TREE=1): measured slower than render_kernel's entry loop on
+  // both list-world configs (MI355X: C5 3840x2159 4x4 97.2 ms vs 78.4; C3 800x800 10x10 24.7 vs 19.1)
+  const bool world_tree = !world_step && getenv("RT_WORLD_TREE") && atoi(getenv("RT_WORLD_TREE")) != 0 &&
                           build_world_tree(s, prims, nodes, wleaf, wxf, wt_fb, w_media, w_inert);
   std::vector<uint32_t> qnodes;
   int q_pairs = 0, q_ebias = 0;
@@ -3841,8 +3944,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   // Split samples of the longest items (stepwise kernel; scheduled launches of a configuration
   // with split items): the launch after the measuring one records their sample-start RNG states,
   // later launches with the same seed run each of their samples as a separate work item.
-  const bool split_ok = have_perm && c->n_split > 0 && (kVariants[var].mask & F_STEP) != 0 && a->spp > 1 &&
-                        (a->flags & RT_FLAG_NO_SPLIT) == 0;
+  const bool split_ok = have_perm && c->n_split > 0 && a->spp > 1 && (a->flags & RT_FLAG_NO_SPLIT) == 0;
   int split_mode = 0;
   if (split_ok && c->split_state == 1 && c->split_seed == a->seed) split_mode = 2;
   else if (split_ok) split_mode = 1;
