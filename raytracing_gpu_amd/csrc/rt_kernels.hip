@@ -1252,6 +1252,9 @@ __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray&
   float lo = tmin, hi = tmax, t1 = 0.0f;
   if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {
       if constexpr ((F & F_STATS) == 0) {  // stats variants run the reference's two queries to count them
+        // an inert medium (o.c = 1 at upload: a bounded sphere boundary, H1) returns before its draw
+        // for every sane ray: its boundary query cannot produce the NaN root that would reach it
+        if (o.c == 1 && ray_sane(r)) return false;
         const rt_object bo = S.objects[o.a];
         const bool prim_leaf = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].kind == RT_OBJ_PRIM : bo.kind == RT_OBJ_PRIM;
         if (prim_leaf) {
@@ -3427,6 +3430,22 @@ bool object_box(const rt_scene_soa* s, int oi, float t0, float t1, rth::Box& out
 // as their t_max), except inert ones: a medium bounded by a sphere never reaches its draw (H1: the
 // second boundary query returns nothing or t1 itself) unless its boundary root is NaN, which a
 // sane ray (ray_sane) cannot produce.  Leaves: 4 float4 each (see DScene::wleaf).
+// A constant medium that never reaches its RNG draw for a sane ray (ray_sane): its boundary is a
+// sphere (or a moving sphere with time1 != time0) with coordinates and radius below 1e6, whose second
+// boundary query repeats the first root (H1, sphere.h:51) -- see sphere_boundary_no_hit.
+static bool medium_inert(const rt_scene_soa* s, const rt_object& o) {
+  if (o.kind != RT_OBJ_MEDIUM || o.a < 0 || o.a >= s->n_objects) return false;
+  const rt_object& bo = s->objects[o.a];
+  if (bo.kind != RT_OBJ_PRIM) return false;
+  const rt_prim& q = s->prims[bo.a];
+  const int ty = q.type & 0xff;
+  if (ty != RT_PRIM_SPHERE && ty != RT_PRIM_MOVING_SPHERE) return false;
+  const int np = ty == RT_PRIM_SPHERE ? 4 : 9;
+  for (int k = 0; k < np; ++k)
+    if (!(std::fabs(q.p[k]) < 1e6f)) return false;
+  return ty == RT_PRIM_SPHERE || q.p[8] != 0.0f;
+}
+
 static bool build_world_tree(const rt_scene_soa* s, const std::vector<rt_prim>& prims, std::vector<rt_bvh_node>& nodes,
                              std::vector<float4>& wleaf, std::vector<float4>& wxf, int& wt_fb, int& w_media,
                              int& w_inert) {
@@ -3442,15 +3461,8 @@ static bool build_world_tree(const rt_scene_soa* s, const std::vector<rt_prim>& 
     const rt_object& o = obj(s->world[w]);
     if (o.kind == RT_OBJ_MEDIUM) {
       const rt_object& bo = obj(o.a);
-      if (w < last_tree) {  // must be inert: a bounded static sphere, or a moving one with t1 > t0
-        if (bo.kind != RT_OBJ_PRIM) return false;
-        const rt_prim& q = s->prims[bo.a];
-        const int ty = q.type & 0xff;
-        if (ty != RT_PRIM_SPHERE && ty != RT_PRIM_MOVING_SPHERE) return false;
-        const int np = ty == RT_PRIM_SPHERE ? 4 : 9;
-        for (int k = 0; k < np; ++k)
-          if (!(std::fabs(q.p[k]) < 1e6f)) return false;
-        if (ty == RT_PRIM_MOVING_SPHERE && !(q.p[8] != 0.0f)) return false;
+      if (w < last_tree) {  // must be inert
+        if (!medium_inert(s, o)) return false;
         w_inert = 1;
       } else if (!(bo.kind == RT_OBJ_PRIM || (bo.kind == RT_OBJ_XFORM && obj(bo.a).kind == RT_OBJ_PRIM))) {
         return false;  // active media: primitive boundaries (object_query's direct path)
@@ -3636,6 +3648,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   std::vector<float2> pmargin(s->n_prims, make_float2(-INFINITY, -INFINITY));
   for (rt_object& o : objects) {
     o.c = -1;
+    if (o.kind == RT_OBJ_MEDIUM && medium_inert(s, o)) o.c = 1;  // object_query skips it for sane rays
     if (o.kind == RT_OBJ_BVH) {
       const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes, pmargin);
       if (fast < 0) return fail(c, RT_ERR_SCENE, "malformed reference bvh");

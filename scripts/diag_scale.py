@@ -19,7 +19,9 @@ import raytracing_gpu_amd as rt
 
 scene, W, H, spp, nfb = (sys.argv[1], *[int(x) for x in sys.argv[2:6]]) if len(sys.argv) > 1 else ("big1", 1200, 800, 10, 10)
 ctx = rt.Context(0)
-ctx.upload(rt.Scene.builtin(scene))
+from bench import scene_assets  # noqa: E402  (door mesh fixture, synthetic textures for C4 / C5)
+
+ctx.upload(rt.Scene.builtin(scene, **scene_assets(scene)[0]))
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
 
