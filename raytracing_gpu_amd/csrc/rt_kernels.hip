@@ -104,7 +104,7 @@ struct DScene {
   int32_t wt_fb;
   int32_t w_media;
   int32_t w_inert;
-  int32_t pad_w;
+  int32_t defer_ok;      // world_hit may defer BVH validation to the final winner (no drawing media)
   // F_QLDS: the world BVH's traversal tree as 24-byte pair records (build_qtree), staged in LDS;
   // q_ebias: exponent bias of their 5-bit per-axis scales
   const uint32_t* qnodes;
@@ -974,7 +974,8 @@ __device__ __forceinline__ bool chain_ok(const DScene& S, int base, int rows, co
 template <int F>
 __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, const Ray& r, float tmin, float tmax,
                                            bool overflow, float bhi, float second, float& best, int& best_prim,
-                                           int best_rank, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+                                           int best_rank, unsigned& nnode, unsigned& nprim, unsigned& nfall,
+                                           bool defer = false) {
   // the reference's reciprocals (three IEEE divides), only on the rare paths that test boxes
   auto inv_of = [&r]() { return mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z); };
   // The candidate search keeps ranges: its winner is certain when every other candidate's range
@@ -1011,6 +1012,7 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
     return pe >= 0;
   }
   if (best_prim < 0) return false;
+  if (defer) return true;  // the caller validates the world query's final winner only (world_hit)
   if (chain_ok<F>(S, base, rows, r, tmin, tmax, best, best_prim, best_rank, nnode)) return true;
   if constexpr ((F & F_STATS) != 0) ++nfall;
   return bvh_exact<F>(S, base, rows, r, inv_of(), tmin, tmax, best, best_prim, nnode, nprim, nfall);
@@ -1079,7 +1081,7 @@ __device__ __forceinline__ int world_settle(const DScene& S, const Ray& r, float
 //     floating-point edge of the reference's own boxes), the query is re-run on the exact visit set.
 template <int F>
 __device__ __forceinline__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, float tmin, float tmax, float& best,
-                            int& best_prim, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+                            int& best_prim, unsigned& nnode, unsigned& nprim, unsigned& nfall, bool defer = false) {
   const int base = o.a, rows = o.b;
   if constexpr ((F & F_EXACT) != 0) {
     const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);  // the reference's reciprocals
@@ -1109,7 +1111,7 @@ __device__ __forceinline__ bool bvh_closest(const DScene& S, const rt_object& o,
     RT_STAMP(5);
     best = blo;
     return bvh_settle<F>(S, base, rows, r, tmin, tmax, overflow, bhi, second, best, best_prim, best_rank, nnode, nprim,
-                         nfall);
+                         nfall, defer);
   }
 }
 
@@ -1117,9 +1119,9 @@ __device__ __forceinline__ bool bvh_closest(const DScene& S, const rt_object& o,
 // shrinking t_max, later object wins ties (hittable_list.h:23-39).
 template <int F>
 __device__ __forceinline__ bool leaf_closest(const DScene& S, const rt_object& o, const Ray& r, float tmin, float tmax, float& t,
-                             int& prim, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+                             int& prim, unsigned& nnode, unsigned& nprim, unsigned& nfall, bool defer = false) {
   if constexpr ((F & F_BVH) != 0)
-    if (o.kind == RT_OBJ_BVH) return bvh_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall);
+    if (o.kind == RT_OBJ_BVH) return bvh_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall, defer);
   if (o.kind == RT_OBJ_PRIM || (F & F_LIST) == 0) {
     prim = o.a;
     return prim_t<F>(S, o.a, r, tmin, tmax, t, nprim);
@@ -1245,7 +1247,8 @@ __device__ __forceinline__ bool medium_hit(const rt_object& o, const Ray& r, flo
 // pointers from there on every use (C5: ~160 scratch loads in the kernel body).
 template <int F>
 __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t,
-                                             int& prim, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
+                                             int& prim, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall,
+                                             bool defer = false) {
   const float inf = __builtin_inff();
   const rt_object o = S.objects[oi];
   int phase = 2, target = oi;
@@ -1305,7 +1308,7 @@ __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray&
     }
     float tq;
     int pq;
-    const bool hit = leaf_closest<F>(S, x, rr, lo, hi, tq, pq, nnode, nprim, nfall);
+    const bool hit = leaf_closest<F>(S, x, rr, lo, hi, tq, pq, nnode, nprim, nfall, defer && phase == 2);
     if (phase == 2) {
       t = tq;
       prim = pq;
@@ -1359,21 +1362,63 @@ __device__ __forceinline__ void object_record(const DScene& S, int oi, int prim,
 
 // World = hittable_list of top-level objects (render.h:63 with t in [0.001, inf)).
 // mask: bit w clear = no ray of this query's set can reach entry w (w < 32; camera-ray tile masks).
+// Deferred validation (S.defer_ok: the list has no medium that draws with the closest hit so far as
+// its t_max, every medium being inert; a sane ray skips those): a BVH entry's candidate is taken
+// without its reference-chain check, and only the final winner's chain is validated, against the
+// t_max the list passed to its entry.  An unvalidated candidate that the reference would reject
+// only lowered the t_max of the entries after it: the final winner W has t_W <= that t_max, the
+// reference's larger t_max for W (and for any entry it passed over) finds the same t_W, and a chain
+// that passes for the smaller t_max passes for the larger.  If W's chain check fails, the whole
+// query runs again with every entry validated.  C5: 25 % of the loop's time was validation +
+// finalize, over three BVH entries per query.
 template <int F>
 __device__ __forceinline__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall,
                           uint32_t mask) {
-  float closest = __builtin_inff();
-  int wobj = -1, wprim = -1;
-  for (int w = 0; w < S.n_world; ++w) {
-    if (w < 32 && ((mask >> w) & 1u) == 0) continue;
-    float t;
-    int pr;
-    const int oi = S.world[w];
-    if (object_query<F>(S, oi, r, 0.001f, closest, t, pr, rng, nnode, nprim, nfall)) {
-      closest = t;
-      wobj = oi;
-      wprim = pr;
+#ifdef RT_NO_DEFER_CODE  // experiment: the world query without the deferred-validation code
+  constexpr bool kDefer = false;
+#else
+  constexpr bool kDefer = (F & (F_STATS | F_CHECK | F_EXACT)) == 0 && (F & F_BVH) != 0;
+#endif
+  bool defer = kDefer && S.defer_ok && ray_sane(r);
+  float closest;
+  int wobj, wprim;
+  for (;;) {
+    closest = __builtin_inff();
+    wobj = -1;
+    wprim = -1;
+    float wtmax = closest;  // the t_max the list passed to the winner's entry
+    for (int w = 0; w < S.n_world; ++w) {
+      if (w < 32 && ((mask >> w) & 1u) == 0) continue;
+      float t;
+      int pr;
+      const int oi = S.world[w];
+      if (object_query<F>(S, oi, r, 0.001f, closest, t, pr, rng, nnode, nprim, nfall, defer)) {
+        wtmax = closest;
+        closest = t;
+        wobj = oi;
+        wprim = pr;
+      }
     }
+    if constexpr (kDefer) {
+      if (defer && wobj >= 0) {
+        const rt_object o = S.objects[wobj];
+        Ray rr = r;
+        int xb = wobj;
+        if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {
+          Ray moved;
+          rr = xform_ray(o, r, moved);
+          xb = o.a;
+        }
+        const rt_object x = S.objects[xb];
+        if (x.kind == RT_OBJ_BVH &&
+            !chain_ok<F>(S, x.a, x.b, rr, 0.001f, wtmax, closest, wprim, __float_as_int(load_prim<F>(S, wprim).c.y),
+                         nnode)) {
+          defer = false;  // the reference may reject it: every entry again, validated
+          continue;
+        }
+      }
+    }
+    break;
   }
   if (wobj < 0) return false;
   object_record<F>(S, wobj, wprim, r, 0.001f, closest, h);
@@ -1704,7 +1749,10 @@ void render_kernel(const RenderParams P) {
   unsigned& item_segs = cold_ref<PK>(item_segs_r, lk + 9 * LB);
   unsigned& nseg = cold_ref<PK>(nseg_r, lk + 10 * LB);
   unsigned& nsamp = cold_ref<PK>(nsamp_r, lk + 11 * LB);
-  // split samples (see render_step_kernel): the item ends after sample s_end - 1; ck = the split claim
+  // split samples (see render_step_kernel; the parking variants only -- C5's, whose shares run on 8
+  // GPUs; C3's variant measured 2.6 % slower with the code and is a one-GPU config): the item ends
+  // after sample s_end - 1; ck = the split claim
+  constexpr bool SPL = PK;
   int s_end_r = 0, ck_r = -1;
   int& s_end = cold_ref<PK>(s_end_r, lk + 21 * LB);
   int& ck = cold_ref<PK>(ck_r, lk + 22 * LB);
@@ -1754,8 +1802,8 @@ void render_kernel(const RenderParams P) {
         } else {
           unsigned long long pos = mine;
           int sa = 0;
-          ck = -1;
-          if (P.split_mode == 2) {  // split samples and the other items, claimed in one sequence
+          if constexpr (SPL) ck = -1;
+          if (SPL && P.split_mode == 2) {  // split samples and the other items, claimed in one sequence
             const unsigned long long nsub = P.n_split * (unsigned long long)P.spp;
             const unsigned long long v = P.order ? (unsigned long long)P.order[mine] : mine;
             if (v < nsub) {
@@ -1765,7 +1813,7 @@ void render_kernel(const RenderParams P) {
             } else {
               pos = v - nsub + P.n_split;
             }
-          } else if (P.split_mode == 1 && mine < P.n_split) {
+          } else if (SPL && P.split_mode == 1 && mine < P.n_split) {
             ck = (int)mine;
           }
           item = P.perm ? (long long)P.perm[pos] : (long long)pos;
@@ -1786,7 +1834,7 @@ void render_kernel(const RenderParams P) {
           const uint4 s0 = st[0], s1 = st[1];
           loc.d = s0.x; loc.v[0] = s0.y; loc.v[1] = s0.z; loc.v[2] = s0.w; loc.v[3] = s1.x; loc.v[4] = s1.y;
           s = sa;
-          s_end = (P.split_mode == 2 && ck >= 0) ? sa + 1 : P.spp;
+          if constexpr (SPL) s_end = (P.split_mode == 2 && ck >= 0) ? sa + 1 : P.spp;
           depth = 0;
           item_segs = 0;
           if constexpr (parks<F>()) {
@@ -1806,7 +1854,7 @@ void render_kernel(const RenderParams P) {
       // ---- begin a sample: jitter + camera ray (render.h:105-108, camera.h:49-58)
       if (depth == 0) {
         RT_STAMP(1);
-        if (P.split_mode == 1 && ck >= 0 && s > 0) {  // record the sample-start state for split launches
+        if (SPL && P.split_mode == 1 && ck >= 0 && s > 0) {  // record the sample-start state for split launches
           uint4* dst = P.ckpt + 2 * ((long long)ck * P.spp + s);
           dst[0] = make_uint4(loc.d, loc.v[0], loc.v[1], loc.v[2]);
           dst[1] = make_uint4(loc.v[3], loc.v[4], item_segs, 0u);
@@ -1876,8 +1924,8 @@ void render_kernel(const RenderParams P) {
         }
         depth = 0;
         ++nsamp;
-        if (++s == s_end) {
-          if (P.split_mode == 2 && ck >= 0) {  // one sample of a split item: its sum, merged later
+        if (++s == (SPL ? s_end : P.spp)) {
+          if (SPL && P.split_mode == 2 && ck >= 0) {  // one sample of a split item: its sum, merged later
             float* dst = P.contrib + 3 * (long long)ck;
             dst[0] = col.x;
             dst[1] = col.y;
@@ -1893,7 +1941,7 @@ void render_kernel(const RenderParams P) {
             dst[1] = out.y;
             dst[2] = out.z;
           }
-          if (P.split_mode == 1 && ck >= 0) P.ckpt[2 * (long long)ck * P.spp + 1] = make_uint4(0u, 0u, item_segs, 0u);
+          if (SPL && P.split_mode == 1 && ck >= 0) P.ckpt[2 * (long long)ck * P.spp + 1] = make_uint4(0u, 0u, item_segs, 0u);
           if (P.row_cost && (i & 15) == 0) atomicAdd(&P.row_cost[j], (unsigned long long)item_segs);  // a sample ranks rows
           if (P.item_cost) P.item_cost[item] = (uint16_t)(item_segs < 65535u ? item_segs : 65535u);
           item = -1;
@@ -3712,6 +3760,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   d.wt_fb = wt_fb;
   d.w_media = w_media;
   d.w_inert = w_inert;
+  d.defer_ok = getenv("RT_NO_DEFER") ? 0 : 1;  // (env: A/B experiments)
+  for (int k = 0; k < s->n_objects; ++k)
+    if (s->objects[k].kind == RT_OBJ_MEDIUM && !medium_inert(s, s->objects[k])) d.defer_ok = 0;
   if (q_pairs > 0 && (rc = upload(c, qnodes.data(), qnodes.size(), &d.qnodes))) return rc;
   d.q_pairs = q_pairs;
   d.q_ebias = q_ebias;
@@ -3957,7 +4008,9 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   // Split samples of the longest items (stepwise kernel; scheduled launches of a configuration
   // with split items): the launch after the measuring one records their sample-start RNG states,
   // later launches with the same seed run each of their samples as a separate work item.
-  const bool split_ok = have_perm && c->n_split > 0 && a->spp > 1 && (a->flags & RT_FLAG_NO_SPLIT) == 0;
+  // (split samples: the stepwise kernel, and render_kernel's parking variants)
+  const bool split_ok = have_perm && c->n_split > 0 && a->spp > 1 && (a->flags & RT_FLAG_NO_SPLIT) == 0 &&
+                        ((kVariants[var].mask & F_STEP) != 0 || parks_segment_mask(kVariants[var].mask));
   int split_mode = 0;
   if (split_ok && c->split_state == 1 && c->split_seed == a->seed) split_mode = 2;
   else if (split_ok) split_mode = 1;

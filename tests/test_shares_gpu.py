@@ -212,10 +212,11 @@ def test_multi_rccl_one_rank_matches_draw(rtlib):
 @pytest.mark.parametrize("band", [None, (4, 1, 3)], ids=["full", "share"])
 @pytest.mark.parametrize("scene", ["cornell_smoke", "final"])
 def test_list_world_split_samples_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch, scene, band, min_segs, cam):
-    """Split samples in render_kernel (C3 / C5 shares): launch 1 measures, launch 2 records the
-    sample-start RNG states of the longest items, launches 3+ run their samples as separate work
-    items and merge them in sample order.  Every launch equals the oracle bit for bit, in both camera
-    modes, full frame and share, at the product's threshold and with every item split."""
+    """Split samples in render_kernel's parking variants (C5's F_FINAL; cornell_smoke through the
+    widest global-memory variant F_ALL, as C3's own narrow variant does not split): launch 1 measures, launch 2
+    records the sample-start RNG states of the longest items, launches 3+ run their samples as separate
+    work items and merge them in sample order.  Every launch equals the oracle bit for bit, in both
+    camera modes, full frame and share, at the product's threshold and with every item split."""
     if min_segs:
         monkeypatch.setenv("RT_SPLIT_MIN_SEGMENTS", min_segs)
     pa, oa = _assets(scene, (341, 152))
@@ -226,7 +227,8 @@ def test_list_world_split_samples_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch,
     band = band or (H, 0, 1)
     import torch
 
-    args = rtlib.make_args(W, H, spp, 0, nfb, 50, cam, band_rows=band[0], band_first=band[1], band_stride=band[2])
+    args = rtlib.make_args(W, H, spp, 0, nfb, 50, cam, band_rows=band[0], band_first=band[1], band_stride=band[2],
+                           widest=scene == "cornell_smoke", lds=scene != "cornell_smoke")
     rows = rtlib.owned_rows(args)
     seen = set()
     for launch in range(4):
