@@ -15,8 +15,10 @@ c5ms2 RT_HIP_LIB=build/ab/libms2.so $C5
 c5r8 RT_HIP_LIB=build/ab/librefill8.so $C5
 c5r24 RT_HIP_LIB=build/ab/librefill24.so $C5
 c5r32 RT_HIP_LIB=build/ab/librefill32.so $C5
+c5ecull RT_HIP_LIB=build/ab/libecull.so $C5
 c5_b $C5
 c3 $C3
+c3ecull RT_HIP_LIB=build/ab/libecull.so $C3
 c3ms RT_HIP_LIB=build/ab/libms.so $C3
 c3ms2 RT_HIP_LIB=build/ab/libms2.so $C3
 c3r8 RT_HIP_LIB=build/ab/librefill8.so $C3
