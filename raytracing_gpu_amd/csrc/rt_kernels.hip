@@ -104,7 +104,7 @@ struct DScene {
   int32_t wt_fb;
   int32_t w_media;
   int32_t w_inert;
-  int32_t defer_ok;      // world_hit may defer BVH validation to the final winner (no drawing media)
+  int32_t pad_w;
   // F_QLDS: the world BVH's traversal tree as 24-byte pair records (build_qtree), staged in LDS;
   // q_ebias: exponent bias of their 5-bit per-axis scales
   const uint32_t* qnodes;
@@ -974,8 +974,7 @@ __device__ __forceinline__ bool chain_ok(const DScene& S, int base, int rows, co
 template <int F>
 __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, const Ray& r, float tmin, float tmax,
                                            bool overflow, float bhi, float second, float& best, int& best_prim,
-                                           int best_rank, unsigned& nnode, unsigned& nprim, unsigned& nfall,
-                                           bool defer = false) {
+                                           int best_rank, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   // the reference's reciprocals (three IEEE divides), only on the rare paths that test boxes
   auto inv_of = [&r]() { return mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z); };
   // The candidate search keeps ranges: its winner is certain when every other candidate's range
@@ -1012,7 +1011,6 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
     return pe >= 0;
   }
   if (best_prim < 0) return false;
-  if (defer) return true;  // the caller validates the world query's final winner only (world_hit)
   if (chain_ok<F>(S, base, rows, r, tmin, tmax, best, best_prim, best_rank, nnode)) return true;
   if constexpr ((F & F_STATS) != 0) ++nfall;
   return bvh_exact<F>(S, base, rows, r, inv_of(), tmin, tmax, best, best_prim, nnode, nprim, nfall);
@@ -1081,7 +1079,7 @@ __device__ __forceinline__ int world_settle(const DScene& S, const Ray& r, float
 //     floating-point edge of the reference's own boxes), the query is re-run on the exact visit set.
 template <int F>
 __device__ __forceinline__ bool bvh_closest(const DScene& S, const rt_object& o, const Ray& r, float tmin, float tmax, float& best,
-                            int& best_prim, unsigned& nnode, unsigned& nprim, unsigned& nfall, bool defer = false) {
+                            int& best_prim, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   const int base = o.a, rows = o.b;
   if constexpr ((F & F_EXACT) != 0) {
     const V inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);  // the reference's reciprocals
@@ -1111,7 +1109,7 @@ __device__ __forceinline__ bool bvh_closest(const DScene& S, const rt_object& o,
     RT_STAMP(5);
     best = blo;
     return bvh_settle<F>(S, base, rows, r, tmin, tmax, overflow, bhi, second, best, best_prim, best_rank, nnode, nprim,
-                         nfall, defer);
+                         nfall);
   }
 }
 
@@ -1119,9 +1117,9 @@ __device__ __forceinline__ bool bvh_closest(const DScene& S, const rt_object& o,
 // shrinking t_max, later object wins ties (hittable_list.h:23-39).
 template <int F>
 __device__ __forceinline__ bool leaf_closest(const DScene& S, const rt_object& o, const Ray& r, float tmin, float tmax, float& t,
-                             int& prim, unsigned& nnode, unsigned& nprim, unsigned& nfall, bool defer = false) {
+                             int& prim, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   if constexpr ((F & F_BVH) != 0)
-    if (o.kind == RT_OBJ_BVH) return bvh_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall, defer);
+    if (o.kind == RT_OBJ_BVH) return bvh_closest<F>(S, o, r, tmin, tmax, t, prim, nnode, nprim, nfall);
   if (o.kind == RT_OBJ_PRIM || (F & F_LIST) == 0) {
     prim = o.a;
     return prim_t<F>(S, o.a, r, tmin, tmax, t, nprim);
@@ -1247,8 +1245,7 @@ __device__ __forceinline__ bool medium_hit(const rt_object& o, const Ray& r, flo
 // pointers from there on every use (C5: ~160 scratch loads in the kernel body).
 template <int F>
 __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t,
-                                             int& prim, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall,
-                                             bool defer = false) {
+                                             int& prim, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   const float inf = __builtin_inff();
   const rt_object o = S.objects[oi];
   int phase = 2, target = oi;
@@ -1308,7 +1305,7 @@ __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray&
     }
     float tq;
     int pq;
-    const bool hit = leaf_closest<F>(S, x, rr, lo, hi, tq, pq, nnode, nprim, nfall, defer && phase == 2);
+    const bool hit = leaf_closest<F>(S, x, rr, lo, hi, tq, pq, nnode, nprim, nfall);
     if (phase == 2) {
       t = tq;
       prim = pq;
@@ -1362,63 +1359,21 @@ __device__ __forceinline__ void object_record(const DScene& S, int oi, int prim,
 
 // World = hittable_list of top-level objects (render.h:63 with t in [0.001, inf)).
 // mask: bit w clear = no ray of this query's set can reach entry w (w < 32; camera-ray tile masks).
-// Deferred validation (S.defer_ok: the list has no medium that draws with the closest hit so far as
-// its t_max, every medium being inert; a sane ray skips those): a BVH entry's candidate is taken
-// without its reference-chain check, and only the final winner's chain is validated, against the
-// t_max the list passed to its entry.  An unvalidated candidate that the reference would reject
-// only lowered the t_max of the entries after it: the final winner W has t_W <= that t_max, the
-// reference's larger t_max for W (and for any entry it passed over) finds the same t_W, and a chain
-// that passes for the smaller t_max passes for the larger.  If W's chain check fails, the whole
-// query runs again with every entry validated.  C5: 25 % of the loop's time was validation +
-// finalize, over three BVH entries per query.
 template <int F>
 __device__ __forceinline__ bool world_hit(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall,
                           uint32_t mask) {
-#ifdef RT_NO_DEFER_CODE  // experiment: the world query without the deferred-validation code
-  constexpr bool kDefer = false;
-#else
-  constexpr bool kDefer = (F & (F_STATS | F_CHECK | F_EXACT)) == 0 && (F & F_BVH) != 0;
-#endif
-  bool defer = kDefer && S.defer_ok && ray_sane(r);
-  float closest;
-  int wobj, wprim;
-  for (;;) {
-    closest = __builtin_inff();
-    wobj = -1;
-    wprim = -1;
-    float wtmax = closest;  // the t_max the list passed to the winner's entry
-    for (int w = 0; w < S.n_world; ++w) {
-      if (w < 32 && ((mask >> w) & 1u) == 0) continue;
-      float t;
-      int pr;
-      const int oi = S.world[w];
-      if (object_query<F>(S, oi, r, 0.001f, closest, t, pr, rng, nnode, nprim, nfall, defer)) {
-        wtmax = closest;
-        closest = t;
-        wobj = oi;
-        wprim = pr;
-      }
+  float closest = __builtin_inff();
+  int wobj = -1, wprim = -1;
+  for (int w = 0; w < S.n_world; ++w) {
+    if (w < 32 && ((mask >> w) & 1u) == 0) continue;
+    float t;
+    int pr;
+    const int oi = S.world[w];
+    if (object_query<F>(S, oi, r, 0.001f, closest, t, pr, rng, nnode, nprim, nfall)) {
+      closest = t;
+      wobj = oi;
+      wprim = pr;
     }
-    if constexpr (kDefer) {
-      if (defer && wobj >= 0) {
-        const rt_object o = S.objects[wobj];
-        Ray rr = r;
-        int xb = wobj;
-        if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {
-          Ray moved;
-          rr = xform_ray(o, r, moved);
-          xb = o.a;
-        }
-        const rt_object x = S.objects[xb];
-        if (x.kind == RT_OBJ_BVH &&
-            !chain_ok<F>(S, x.a, x.b, rr, 0.001f, wtmax, closest, wprim, __float_as_int(load_prim<F>(S, wprim).c.y),
-                         nnode)) {
-          defer = false;  // the reference may reject it: every entry again, validated
-          continue;
-        }
-      }
-    }
-    break;
   }
   if (wobj < 0) return false;
   object_record<F>(S, wobj, wprim, r, 0.001f, closest, h);
@@ -1623,7 +1578,9 @@ constexpr int kBlock = 256;
 constexpr int kAuditCap = 4096;
 constexpr int kTileShift = 3;  // camera-ray candidate lists per 8x8-pixel tile
 constexpr int kTileCap = 32;   // entries per tile list (a fuller tile traverses the tree)
-constexpr int kRefill = 16;  // refill a wave once this many lanes are idle
+// render_kernel refills a wave once this many lanes are idle (same box, Mrays/s at 16 / 8 / 4 / 2 / 1:
+// C3 18 854 / 20 165 / 20 590 / 20 571 / 20 645, C5 3 749 / 3 829 / 3 828 / 3 813 / 3 745)
+constexpr int kRefill = 4;
 constexpr int kShadeMin = 60;  // render_step_kernel: default shading-phase threshold
 constexpr int kShadeMinMesh = 48;  // ... for triangle-mesh variants
 #ifndef RT_SHADE_PASSES
@@ -3760,9 +3717,6 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   d.wt_fb = wt_fb;
   d.w_media = w_media;
   d.w_inert = w_inert;
-  d.defer_ok = getenv("RT_NO_DEFER") ? 0 : 1;  // (env: A/B experiments)
-  for (int k = 0; k < s->n_objects; ++k)
-    if (s->objects[k].kind == RT_OBJ_MEDIUM && !medium_inert(s, s->objects[k])) d.defer_ok = 0;
   if (q_pairs > 0 && (rc = upload(c, qnodes.data(), qnodes.size(), &d.qnodes))) return rc;
   d.q_pairs = q_pairs;
   d.q_ebias = q_ebias;
