@@ -63,6 +63,7 @@ enum : int {
   F_STEP = 1 << 14,   // world = one BVH object: render_step_kernel (one traversal step per loop trip)
   F_WORLD = 1 << 15,  // list world flattened into ONE traversal tree (render_step_kernel; rt_scene_upload)
   F_QLDS = 1 << 16,   // the world BVH's traversal tree quantized to 24-byte pair records in LDS (qpair)
+  F_MERGE = 1 << 17,  // render_kernel answers world queries with world_search only (merge_ok scenes)
   F_ALL = (1 << 11) - 2,
   F_SPHERES = F_MOVING | F_CHECKER | F_BVH,           // basic, first, big1 (C2), two_spheres
   F_CORNELL = F_RECT | F_LIST | F_XFORM | F_MEDIUM,   // cornell, cornell_smoke (C3)
@@ -104,7 +105,7 @@ struct DScene {
   int32_t wt_fb;
   int32_t w_media;
   int32_t w_inert;
-  int32_t pad_w;
+  int32_t merge_ok;      // render_kernel may answer world queries with world_search
   // F_QLDS: the world BVH's traversal tree as 24-byte pair records (build_qtree), staged in LDS;
   // q_ebias: exponent bias of their 5-bit per-axis scales
   const uint32_t* qnodes;
@@ -773,11 +774,13 @@ __device__ __forceinline__ void qpair(const DScene& S, int cur, V oi, V finv, fl
   c1 = (int)(short)(c.y >> 16);
 }
 
-template <int F>
+// KEYED (world_search): candidates carry the tie key kbase | reference leaf rank of their list entry
+// and follow take_candidate<true>'s cross-entry rule.
+template <int F, bool KEYED = false>
 __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r, V oi, V finv, float a, float rcpa,
                                           float tmin, float tmax, int& cur, int& sp, float& blo, float& bhi,
                                           float& second, int& best_prim, int& best_rank, bool& overflow,
-                                          unsigned& nnode, unsigned& nprim) {
+                                          unsigned& nnode, unsigned& nprim, int kbase = 0) {
   stack_t<F>* stk = stack_of<F>(S);
   constexpr int BS = render_block<F>();
   RT_STAMP(3);
@@ -832,8 +835,12 @@ __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r,
         } else {
           const PrimRec q = load_prim<F>(S, pi);
           float lo, hi;
-          if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim))
-            take_candidate(lo, hi, pi, __float_as_int(q.c.y), blo, bhi, second, best_prim, best_rank);
+          if (prim_range<F>(S, q, r, a, rcpa, tmin, tmax, lo, hi, nprim)) {
+            if constexpr (KEYED)
+              take_candidate<true>(lo, hi, pi, kbase | __float_as_int(q.c.y), blo, bhi, second, best_prim, best_rank);
+            else
+              take_candidate(lo, hi, pi, __float_as_int(q.c.y), blo, bhi, second, best_prim, best_rank);
+          }
         }
         RT_STAMP(3);
       }
@@ -1380,6 +1387,140 @@ __device__ __forceinline__ bool world_hit(const DScene& S, const Ray& r, Hit& h,
   return true;
 }
 
+// List world as ONE candidate search (S.merge_ok: entries are primitives, BVHs and instances of
+// them, plus inert media; render_kernel's variants without counters).  The entries are visited in
+// list order as world_hit does -- an instance's ray transformed once per entry, a BVH entry through
+// its own traversal tree -- but their candidates go into one (winner, second) pair with list tie keys
+// (take_candidate<true>, key = (n_world - 1 - w) << RT_WKEY_SHIFT | reference leaf rank: a later entry
+// wins an exact tie, inside a BVH the lower rank), every traversal culls against the best candidate
+// of all entries so far, and only the final winner gets its exact root and its reference-chain
+// check, against a lower bound of the t_max the list passes to its entry (world_settle's argument).
+// A sphere entry is a candidate range instead of an IEEE sqrt and divide.  Returns 0: certain miss,
+// 1: certain hit (best, wobj, prim), 2: not certain (the caller runs the exact sequential list).
+template <int F>
+__device__ __forceinline__ int world_search(const DScene& S, const Ray& r, uint32_t mask, float& best, int& wobj,
+                                            int& prim, unsigned& nnode, unsigned& nprim) {
+  const float tmin = 0.001f, inf = __builtin_inff();
+  float blo = inf, bhi = inf, second = inf;
+  int best_prim = -1, best_key = 0x7fffffff;
+  bool overflow = false;
+  const int NW = S.n_world;
+  for (int w = 0; w < NW; ++w) {
+    if (w < 32 && ((mask >> w) & 1u) == 0) continue;
+    const rt_object o = S.objects[S.world[w]];
+    if ((F & F_MEDIUM) != 0 && o.kind == RT_OBJ_MEDIUM) continue;  // inert (merge_ok), the ray is sane
+    Ray rr = r;
+    int xi = S.world[w];
+    if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {
+      Ray moved;
+      rr = xform_ray(o, r, moved);
+      xi = o.a;
+    }
+    const rt_object x = S.objects[xi];
+    const int kbase = (NW - 1 - w) << RT_WKEY_SHIFT;
+    const float a = len2(rr.d), rcpa = __builtin_amdgcn_rcpf(a);
+    if ((F & F_BVH) != 0 && x.kind == RT_OBJ_BVH) {
+      const V inv = mk(__builtin_amdgcn_rcpf(rr.d.x), __builtin_amdgcn_rcpf(rr.d.y), __builtin_amdgcn_rcpf(rr.d.z));
+      const V finv = mk(__builtin_fminf(__builtin_fmaxf(inv.x, -1e30f), 1e30f),
+                        __builtin_fminf(__builtin_fmaxf(inv.y, -1e30f), 1e30f),
+                        __builtin_fminf(__builtin_fmaxf(inv.z, -1e30f), 1e30f));
+      const V oi = mk(rr.o.x * finv.x, rr.o.y * finv.y, rr.o.z * finv.z);
+      int sp = 0, cur = 0;
+      for (;;) {
+        if (!trav_step<F, true>(S, x.c, rr, oi, finv, a, rcpa, tmin, inf, cur, sp, blo, bhi, second, best_prim, best_key,
+                                overflow, nnode, nprim, kbase))
+          break;
+      }
+    } else {
+      const PrimRec q = load_prim<F>(S, x.a);
+      float lo, hi;
+      if (prim_range<F>(S, q, rr, a, rcpa, tmin, inf, lo, hi, nprim))
+        take_candidate<true>(lo, hi, x.a, kbase, blo, bhi, second, best_prim, best_key);
+    }
+  }
+  if (overflow || (best_prim >= 0 && !(second > bhi))) return 2;
+  if (best_prim < 0) return 0;
+  wobj = S.world[NW - 1 - (best_key >> RT_WKEY_SHIFT)];
+  prim = best_prim;
+  const rt_object o = S.objects[wobj];
+  Ray rr = r;
+  int xi = wobj;
+  if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {
+    Ray moved;
+    rr = xform_ray(o, r, moved);
+    xi = o.a;
+  }
+  best = blo;
+  if (blo != bhi) {  // a range: the exact root once
+    unsigned np = 0;
+    if (!prim_t<F>(S, best_prim, rr, tmin, inf, best, np)) return 2;
+  }
+  if constexpr ((F & F_BVH) != 0) {
+    const rt_object x = S.objects[xi];
+    if (x.kind == RT_OBJ_BVH) {
+      const float lim = __builtin_fminf(second, bhi * 1.0009765625f);
+      if (!chain_ok<F>(S, x.a, x.b, rr, tmin, lim, best, best_prim, best_key & ((1 << RT_WKEY_SHIFT) - 1), nnode))
+        return 2;
+    }
+  }
+  return 1;
+}
+
+// render_kernel's world query on merge_ok lists: world_search, and when it is not certain the
+// reference's list loop exactly (render_step_kernel's world branch: exact BVH visit sets, exact
+// primitive roots, the media's own queries).
+template <int F>
+__device__ __forceinline__ bool world_query_merged(const DScene& S, const Ray& r, Hit& h, Rng& rng, unsigned& nnode,
+                                                   unsigned& nprim, unsigned& nfall, uint32_t mask) {
+  float best = 0.0f;
+  int wobj = -1, wprim = -1;
+  int st = ray_sane(r) ? world_search<F>(S, r, mask, best, wobj, wprim, nnode, nprim) : 2;
+  if (S.merge_ok > 1) st = 2;  // RT_MERGE_FALLBACK (tests): every query through the exact list
+  if (st == 0) return false;
+  if (st == 2) {  // every entry in list order, exactly (render_step_kernel's world branch)
+    constexpr int FM = F & ~F_BVH;  // media boundaries are primitives
+    const float tmin = 0.001f;
+    bool hit = false;
+    for (int w = 0; w < S.n_world; ++w) {
+      if (w < 32 && ((mask >> w) & 1u) == 0) continue;
+      const int oi = S.world[w];
+      const rt_object o = S.objects[oi];
+      const float tcl = hit ? best : __builtin_inff();
+      float tq;
+      int pq;
+      bool hq;
+      if ((F & F_MEDIUM) != 0 && o.kind == RT_OBJ_MEDIUM) {
+        hq = object_query<FM>(S, oi, r, tmin, tcl, tq, pq, rng, nnode, nprim, nfall);
+      } else {
+        Ray rr = r;
+        int xi = oi;
+        if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {
+          Ray moved;
+          rr = xform_ray(o, r, moved);
+          xi = o.a;
+        }
+        const rt_object x = S.objects[xi];
+        if ((F & F_BVH) != 0 && x.kind == RT_OBJ_BVH) {
+          hq = bvh_exact<F>(S, x.a, x.b, rr, mk(1.0f / rr.d.x, 1.0f / rr.d.y, 1.0f / rr.d.z), tmin, tcl, tq, pq, nnode,
+                            nprim, nfall);
+        } else {
+          pq = x.a;
+          hq = prim_t<F>(S, x.a, rr, tmin, tcl, tq, nprim);
+        }
+      }
+      if (hq) {
+        hit = true;
+        best = tq;
+        wobj = oi;
+        wprim = pq;
+      }
+    }
+    if (!hit) return false;
+  }
+  object_record<F>(S, wobj, wprim, r, 0.001f, best, h);
+  return true;
+}
+
 // ------------------------------------------------------------------ textures (texture.h, perlin.h)
 __device__ float perlin_noise(const rt_perlin& P, V p) {
   const float u = p.x - __builtin_floorf(p.x), v = p.y - __builtin_floorf(p.y), w = p.z - __builtin_floorf(p.z);
@@ -1838,7 +1979,16 @@ void render_kernel(const RenderParams P) {
       RT_DIAG(2);
       const uint32_t wmask = (depth == 0 && P.tile_mask) ? P.tile_mask[(j >> kTileShift) * P.tiles_x + (i >> kTileShift)]
                                                          : 0xffffffffu;
-      const bool hit_any = world_hit<F>(S, ray, h, loc, nnode, nprim, nfall, wmask);
+      // The merged candidate search on scenes rt_scene_upload marks merge_ok: only it in the F_MERGE
+      // variants (C5: F_FINAL's entry loop costs 11 more spilled VGPRs), decided per scene in the
+      // widest counter-free ones.
+      constexpr bool kOnly = (F & F_MERGE) != 0;
+      constexpr bool kDyn = !kOnly && (F & F_ALL) == F_ALL && (F & (F_STATS | F_EXACT | F_CHECK)) == 0;
+      bool hit_any;
+      if (kOnly || (kDyn && S.merge_ok))
+        hit_any = world_query_merged<((kOnly || kDyn) ? F : 0)>(S, ray, h, loc, nnode, nprim, nfall, wmask);
+      else
+        hit_any = world_hit<F>(S, ray, h, loc, nnode, nprim, nfall, wmask);
       RT_STAMP(6);
   #ifdef RT_TRACE
       if (item == P.trace_item && P.trace) {
@@ -2312,6 +2462,11 @@ void render_step_kernel(const RenderParams P) {
     // ---- traversal steps until shade_min lanes wait (or none traverses)
     for (;;) {
       RT_DIAG(3);
+#ifndef RT_TRAV_UNROLL
+#define RT_TRAV_UNROLL 1
+#endif
+#pragma unroll
+      for (int u = 0; u < RT_TRAV_UNROLL; ++u)
       if (mode == 1) {
         RT_DIAG(0);
         if (!trav_step<F>(S, tbase, ray, oi, finv, qa, rcpa, tmin, tmax, cur, sp, best, bhi, second, best_prim,
@@ -2822,6 +2977,7 @@ const Variant kVariants[] = {
     RT_VARIANT(F_MESH | F_STATS),
     RT_VARIANT(F_MESH | F_EXACT),
     RT_VARIANT(F_FINAL),
+    RT_VARIANT(F_FINAL | F_MERGE),
 #endif
 };
 #undef RT_VARIANT
@@ -2832,8 +2988,8 @@ constexpr int kLdsBudget = 156 * 1024;  // bytes of staged nodes + primitives + 
 
 // Smallest compiled variant that covers the scene's features and the requested mode.
 int pick_variant(int features, bool stats, bool exact, bool check, bool lds, bool widest = false, bool step = false,
-                 bool world = false, bool qlds = false) {
-  const int modes = F_STATS | F_EXACT | F_CHECK | F_LDS | F_STEP | F_WORLD | F_QLDS;
+                 bool world = false, bool qlds = false, bool merge = false) {
+  const int modes = F_STATS | F_EXACT | F_CHECK | F_LDS | F_STEP | F_WORLD | F_QLDS | F_MERGE;
   const int mode = check ? F_CHECK : ((stats ? F_STATS : 0) | (exact ? F_EXACT : 0));
   auto best_of = [&](int want) {  // covering variant with the fewest (widest: most) feature bits
     int best = -1;
@@ -2861,6 +3017,9 @@ int pick_variant(int features, bool stats, bool exact, bool check, bool lds, boo
         if (kVariants[w].mask == (kVariants[sv].mask | F_QLDS)) return w;
     if (sv >= 0) return sv;
   }
+  if (v >= 0 && merge && mode == 0)  // its merged-search twin (render_kernel; merge_ok scenes)
+    for (int w = 0; w < kNumVariants; ++w)
+      if (kVariants[w].mask == (kVariants[v].mask | F_MERGE)) return w;
   return v;
 }
 int variant_block(int v) { return (kVariants[v].mask & (F_LDS | F_QLDS)) != 0 ? 1024 : 256; }
@@ -3717,6 +3876,18 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   d.wt_fb = wt_fb;
   d.w_media = w_media;
   d.w_inert = w_inert;
+  // world_search applies: a list of primitives, BVHs (up to 2^20 leaves) and instances of them, and
+  // inert media (RT_NO_MERGE: the entry loop; A/B experiments)
+  // (RT_MERGE_FALLBACK: the search runs, then every query takes the exact list; tests)
+  d.merge_ok = !world_step && s->n_world >= 2 && s->n_world < (1 << (31 - RT_WKEY_SHIFT)) && !getenv("RT_NO_MERGE");
+  for (int w = 0; w < s->n_world && d.merge_ok; ++w) {
+    const rt_object& o = s->objects[s->world[w]];
+    const rt_object& x = o.kind == RT_OBJ_XFORM ? s->objects[o.a] : o;
+    if (o.kind == RT_OBJ_MEDIUM) d.merge_ok = medium_inert(s, o);
+    else if (x.kind == RT_OBJ_BVH) d.merge_ok = x.b <= RT_WKEY_SHIFT;
+    else d.merge_ok = x.kind == RT_OBJ_PRIM;
+  }
+  if (d.merge_ok && getenv("RT_MERGE_FALLBACK")) d.merge_ok = 2;
   if (q_pairs > 0 && (rc = upload(c, qnodes.data(), qnodes.size(), &d.qnodes))) return rc;
   d.q_pairs = q_pairs;
   d.q_ebias = q_ebias;
@@ -3952,7 +4123,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   const bool step = (c->world_step || c->world_tree) && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
   const bool qlds = !use_lds && c->scene.q_pairs > 0 && (a->flags & RT_FLAG_NO_LDS) == 0;
   const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
-                               (a->flags & RT_FLAG_WIDEST) != 0, step, c->world_tree, qlds);
+                               (a->flags & RT_FLAG_WIDEST) != 0, step, c->world_tree, qlds, c->scene.merge_ok != 0);
   if (var < 0) return fail(c, RT_ERR_SCENE, "no kernel variant covers the scene features");
   // shading phase of render_step_kernel once this many lanes of a wave wait (RT_SHADE_MIN: tuning)
   // (measured: C2 best at 60 of 64 lanes; C4's triangle-mesh steps at 48: 125.0 -> 119.7 ms, 40: 121.8)

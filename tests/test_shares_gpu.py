@@ -243,3 +243,40 @@ def test_list_world_split_samples_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch,
         assert cnt["samples"] == nfb * len(rows) * W * spp
     if min_segs:
         assert rtlib.RT_SCHED_PREVIOUS | rtlib.RT_SCHED_SPLIT_REPLAY in seen
+
+
+@pytest.mark.parametrize("mode", ["merged", "fallback", "entry_loop"])
+@pytest.mark.parametrize("scene", ["final", "first", "two_perlin", "cornell"])
+def test_merged_list_search_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch, scene, mode):
+    """render_kernel's merged list-world search (world_search: every entry's candidates in one
+    winner/second pair with list tie keys, one settle per query; scenes of primitives, BVHs, instances
+    and inert media): C5's own variant on final, the widest global-memory variant F_ALL on the
+    primitive-only lists.  "fallback" (RT_MERGE_FALLBACK) runs the search and then answers every query
+    through the exact entry loop, "entry_loop" (RT_NO_MERGE) is the per-entry world_hit.  Full frame and
+    a share, cold and scheduled launches, against the oracle bit for bit."""
+    if mode == "fallback":
+        monkeypatch.setenv("RT_MERGE_FALLBACK", "1")
+    elif mode == "entry_loop":
+        monkeypatch.setenv("RT_NO_MERGE", "1")
+    pa, oa = _assets(scene, (341, 152))
+    W, H, spp, nfb = (96, 54, 2, 2) if scene != "cornell" else (48, 48, 4, 2)
+    gpu_ctx.upload(rtlib.Scene.builtin(scene, **pa))  # merge_ok is decided at upload
+    ref = oracle.RefScene(scene, **oa)
+    want = [ref.render(W, H, spp, f, 50, REF) for f in range(nfb)]
+    import torch
+
+    for band in ((H, 0, 1), (4, 1, 3)):
+        args = rtlib.make_args(W, H, spp, 0, nfb, 50, REF, band_rows=band[0], band_first=band[1],
+                               band_stride=band[2], widest=scene != "final", lds=scene == "final")
+        rows = rtlib.owned_rows(args)
+        for launch in range(3):
+            gpu_ctx.render_init(W, H, 1984)
+            fb = torch.full((nfb * len(rows) * W * 3,), float("nan"), dtype=torch.float32, device="cuda")
+            cnt = gpu_ctx.render(args, fb.data_ptr())
+            assert gpu_ctx.last_render_kernel().startswith("render_kernel<"), gpu_ctx.last_render_kernel()
+            got = fb.cpu().numpy().reshape(nfb, len(rows), W, 3)
+            for f in range(nfb):
+                diff = (_bits(got[f]) != _bits(want[f][0].reshape(H, W, 3)[rows])).any(axis=2)
+                assert not diff.any(), f"{scene} {mode} band {band} launch {launch} fb {f}: {int(diff.sum())} px"
+            if band[2] == 1:
+                assert cnt["segments"] == sum(int(w[1]["segments"]) for w in want)
