@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <set>
 #include <type_traits>
 #include <cstdio>
 #include <cstring>
@@ -3215,10 +3217,35 @@ int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<
       pmargin[id] = make_float2(mbits, safe);
     }
   }
+  // Coincident triangles (the reference's mesh import indexes the concatenated vertex array with
+  // per-mesh local indices, H16: 1 828 of the door's 4 330 triangles repeat an earlier one's v0, e0,
+  // e1 bit for bit) hit every ray at the same t, so among them the reference keeps the first it
+  // visits in its depth-first left-first order: the lowest leaf rank whose chain passes.  The
+  // candidate search only needs that member; members are in rank order, so the first of each group
+  // stays in the tree.  The settle validates the kept member's chain; if it fails the query re-runs
+  // on the exact visit set, where a later member may win (RT_NO_DEDUP=1 keeps every member).
+  std::vector<int> kept;
+  if (!getenv("RT_NO_DEDUP")) {
+    std::set<std::array<uint32_t, 9>> seen;
+    for (int id : members) {
+      if ((prims[id].type & 0xff) == RT_PRIM_TRIANGLE) {
+        const int ti = (int)prims[id].p[0];
+        if (ti < 0 || ti >= s->n_triangles) return -1;
+        const rt_triangle& t = s->triangles[ti];
+        std::array<uint32_t, 9> key;
+        memcpy(&key[0], t.v0, 12);
+        memcpy(&key[3], t.e0, 12);
+        memcpy(&key[6], t.e1, 12);
+        if (!seen.insert(key).second) continue;
+      }
+      kept.push_back(id);
+    }
+  }
+  std::vector<int>& leaves = kept.size() >= 2 ? kept : members;
   const int fb = (int)nodes.size();
   nodes.resize(fb + 2);  // record 0 = root
   SahBuilder sb{box, nodes, fb};
-  sb.build(members.data(), n, 0);
+  sb.build(leaves.data(), (int)leaves.size(), 0);
   return fb;
 }
 
