@@ -1725,7 +1725,7 @@ constexpr int kTileCap = 32;   // entries per tile list (a fuller tile traverses
 // C3 18 854 / 20 165 / 20 590 / 20 571 / 20 645, C5 3 749 / 3 829 / 3 828 / 3 813 / 3 745)
 constexpr int kRefill = 4;
 constexpr int kShadeMin = 60;  // render_step_kernel: default shading-phase threshold
-constexpr int kShadeMinMesh = 48;  // ... for triangle-mesh variants
+constexpr int kShadeMinMesh = 56;  // ... for triangle-mesh variants (48 before the triangle dedupe)
 #ifndef RT_SHADE_PASSES
 #define RT_SHADE_PASSES 2
 #endif
@@ -4158,6 +4158,8 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   if (var < 0) return fail(c, RT_ERR_SCENE, "no kernel variant covers the scene features");
   // shading phase of render_step_kernel once this many lanes of a wave wait (RT_SHADE_MIN: tuning)
   // (measured: C2 best at 60 of 64 lanes; C4's triangle-mesh steps at 48: 125.0 -> 119.7 ms, 40: 121.8)
+  // (round 4, after the triangle dedupe and two steps per check, C4 Mrays/s at 40/48/52/56/60/62: 13 490 /
+  // 13 922 / 14 052 / 14 090 / 13 932 / 13 618; C2 at 56/60/62: 14 659 / 14 747 / 14 605)
   P.shade_min = (kVariants[var].mask & F_TRI) != 0 ? kShadeMinMesh : kShadeMin;
   P.perm = have_perm ? c->perm : nullptr;
   P.n_long = have_perm ? c->n_long : 0;
