@@ -2464,12 +2464,14 @@ void render_step_kernel(const RenderParams P) {
     // ---- traversal steps until shade_min lanes wait (or none traverses)
     for (;;) {
       RT_DIAG(3);
-      // two traversal steps per check of the shading condition (C2 +1.1 %, C4 +0.6 %, same box; same
-      // VGPRs); the opt-in world-tree variants keep one (more spills with two)
+      // several traversal steps per check of the shading condition, same VGPRs (same box, Mrays/s at
+      // 1 / 2 / 3 / 4 steps: C2 14 538 / 14 713 / 14 829 / 14 843, C4 11 180 / 11 247 (before the
+      // triangle dedupe) and 14 095 / 14 051 / 13 990 after it); the opt-in world-tree variants keep
+      // one (more spills with two)
 #ifdef RT_TRAV_UNROLL
       constexpr int kUnroll = RT_TRAV_UNROLL;
 #else
-      constexpr int kUnroll = (F & F_WORLD) != 0 ? 1 : 2;
+      constexpr int kUnroll = (F & F_WORLD) != 0 ? 1 : ((F & F_TRI) != 0 ? 2 : 4);
 #endif
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u)

@@ -292,6 +292,37 @@ def test_culled_equals_exact_asset_scenes(rtlib, gpu_ctx, scene, W, H, spp, nfb)
     assert not diff.any(), f"{scene}: {int(diff.sum())} floats differ"
 
 
+@pytest.mark.parametrize("scene", ["door", "final"])
+def test_coincident_triangles_leave_the_traversal_tree(rtlib, gpu_ctx, monkeypatch, scene):
+    """The door's H16 duplicates (triangles repeating an earlier one's v0, e0, e1 bit for bit) keep
+    one leaf per group in the traversal trees: every float and the segment count equal the build with
+    every member (RT_NO_DEDUP=1, read at upload) and the exact visit set, with fewer primitive tests."""
+    import os
+
+    import torch
+    from raytracing_gpu_amd import assets
+
+    m = assets.door_mesh_from_fixture(os.path.join(os.path.dirname(__file__), "golden", "door_assimp.npz"))
+    img = assets.synthetic_image(341, 152)
+    W, H, spp, nfb = 320, 180, 4, 2
+    out = {}
+    for mode in ("dedup", "all", "exact"):
+        if mode == "all":
+            monkeypatch.setenv("RT_NO_DEDUP", "1")
+        else:
+            monkeypatch.delenv("RT_NO_DEDUP", raising=False)
+        gpu_ctx.upload(rtlib.Scene.builtin(scene, images=[img], meshes=[m]))
+        gpu_ctx.render_init(W, H, 1984)
+        fb = torch.zeros(nfb * H * W * 3, dtype=torch.float32, device="cuda")
+        cnt = gpu_ctx.render(rtlib.make_args(W, H, spp, 0, nfb, 50, REF, stats=True, exact=mode == "exact"),
+                             fb.data_ptr())
+        out[mode] = (fb.cpu().numpy(), cnt)
+    for mode in ("all", "exact"):
+        assert out[mode][1]["segments"] == out["dedup"][1]["segments"]
+        assert np.array_equal(_bits(out[mode][0]), _bits(out["dedup"][0])), mode
+    assert out["dedup"][1]["prim_tests"] < out["all"][1]["prim_tests"]
+
+
 @pytest.mark.parametrize("scene,W,H,spp,nfb,cam", [
     ("big1", 1200, 800, 10, 10, REF),     # the whole C2 bench workload
     ("big1", 333, 187, 3, 2, PIX),
