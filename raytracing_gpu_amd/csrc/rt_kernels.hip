@@ -117,6 +117,26 @@ struct DScene {
   float bg[3];
 };
 
+// Read-only scene arrays through the constant address space: a load whose address is wave-uniform
+// (a list entry's object and primitive records, the world list) becomes a scalar load into SGPRs
+// instead of a vector load that fills a VGPR with 64 copies; a lane-dependent address still becomes
+// a global_load.  The scene is never written while a kernel runs.
+// Only in variants without BVHs or triangles (C3's list of rects and media, whose entry loop is all
+// uniform loads: 118 -> 108 VGPRs): in C5's variant the records held in SGPRs raise its SGPR spills
+// into VGPR lanes and its VGPR spills (39 -> 49).
+#define RT_RO __attribute__((address_space(4)))
+// (The host pass type-checks device bodies too, and x86 has no address space 4 to copy a record
+// from: there ro is the plain pointer.)
+template <int F, class T>
+__device__ __forceinline__ auto ro(const T* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr ((F & (F_BVH | F_TRI)) == 0) return (const RT_RO T*)p;
+  else return p;
+#else
+  return p;
+#endif
+}
+
 // LDS image of the scene for F_LDS variants: [nodes (2 float4 each) | prims (3 float4 each)].
 extern __shared__ float4 rt_lds[];
 
@@ -353,8 +373,13 @@ struct PrimRec {
 };
 template <int F>
 __device__ __forceinline__ PrimRec load_prim(const DScene& S, int i) {
-  const float4* q = prims_of<F>(S) + 3 * i;
-  return PrimRec{q[0], q[1], q[2]};
+  if constexpr ((F & (F_LDS | F_BVH | F_TRI)) == 0) {  // read-only scene memory (ro): s_load when i is wave-uniform
+    const auto q = ro<F>(S.prims) + 3 * i;
+    return PrimRec{q[0], q[1], q[2]};
+  } else {
+    const float4* q = prims_of<F>(S) + 3 * i;
+    return PrimRec{q[0], q[1], q[2]};
+  }
 }
 __device__ __forceinline__ int prim_type(const PrimRec& q) { return __float_as_int(q.c.z) & RT_PRIM_TYPE_MASK; }
 
@@ -1067,11 +1092,11 @@ __device__ __forceinline__ int world_settle(const DScene& S, const Ray& r, float
   const int bobj = __float_as_int(dw.z);
   prim = __float_as_int(dw.w);
   if (bobj >= 0) {
-    const int base = S.objects[bobj].a, rows = S.objects[bobj].b;
+    const int base = ro<F>(S.objects)[bobj].a, rows = ro<F>(S.objects)[bobj].b;
     const float lim = __builtin_fminf(second, bhi * 1.0009765625f);
     if (!chain_ok<F>(S, base, rows, rr, tmin, lim, best, prim, key & ((1 << RT_WKEY_SHIFT) - 1), nnode)) return 2;
   }
-  wobj = S.world[__float_as_int(dw.y)];
+  wobj = ro<F>(S.world)[__float_as_int(dw.y)];
   return 1;
 }
 
@@ -1169,7 +1194,7 @@ __device__ __forceinline__ Ray xform_ray(const rt_object& o, const Ray& r, Ray& 
 template <int F>
 __device__ __forceinline__ bool sphere_boundary_no_hit(const DScene& S, int boundary, float t1) {
   if constexpr ((F & F_STATS) != 0) return false;
-  const rt_object bo = S.objects[boundary];
+  const rt_object bo = ro<F>(S.objects)[boundary];
   return bo.kind == RT_OBJ_PRIM && t1 == t1 && prim_type(load_prim<F>(S, bo.a)) <= RT_PRIM_MOVING_SPHERE;
 }
 
@@ -1256,7 +1281,7 @@ template <int F>
 __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray& r, float tmin, float tmax, float& t,
                                              int& prim, Rng& rng, unsigned& nnode, unsigned& nprim, unsigned& nfall) {
   const float inf = __builtin_inff();
-  const rt_object o = S.objects[oi];
+  const rt_object o = ro<F>(S.objects)[oi];
   int phase = 2, target = oi;
   float lo = tmin, hi = tmax, t1 = 0.0f;
   if constexpr ((F & F_MEDIUM) != 0) if (o.kind == RT_OBJ_MEDIUM) {
@@ -1264,10 +1289,10 @@ __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray&
         // an inert medium (o.c = 1 at upload: a bounded sphere boundary, H1) returns before its draw
         // for every sane ray: its boundary query cannot produce the NaN root that would reach it
         if (o.c == 1 && ray_sane(r)) return false;
-        const rt_object bo = S.objects[o.a];
-        const bool prim_leaf = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].kind == RT_OBJ_PRIM : bo.kind == RT_OBJ_PRIM;
+        const rt_object bo = ro<F>(S.objects)[o.a];
+        const bool prim_leaf = bo.kind == RT_OBJ_XFORM ? ro<F>(S.objects)[bo.a].kind == RT_OBJ_PRIM : bo.kind == RT_OBJ_PRIM;
         if (prim_leaf) {
-          const int pi = bo.kind == RT_OBJ_XFORM ? S.objects[bo.a].a : bo.a;
+          const int pi = bo.kind == RT_OBJ_XFORM ? ro<F>(S.objects)[bo.a].a : bo.a;
           const PrimRec q = load_prim<F>(S, pi);
           float b1, b2;
           if ((F & F_RECT) != 0 && prim_type(q) == RT_PRIM_BOX)
@@ -1287,12 +1312,12 @@ __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray&
   }
   if constexpr ((F & F_BVH) == 0) {  // no traversal to share (C3): straight-line queries measured faster
     auto leaf_q = [&](int ti, float qlo, float qhi, float& tq, int& pq) {
-      rt_object x = S.objects[ti];
+      rt_object x = ro<F>(S.objects)[ti];
       Ray rr = r;
       if constexpr ((F & F_XFORM) != 0) if (x.kind == RT_OBJ_XFORM) {
           Ray moved;
           rr = xform_ray(x, r, moved);
-          x = S.objects[x.a];
+          x = ro<F>(S.objects)[x.a];
       }
       return leaf_closest<F>(S, x, rr, qlo, qhi, tq, pq, nnode, nprim, nfall);
     };
@@ -1305,12 +1330,12 @@ __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray&
     return medium_hit<F>(o, r, tmin, tmax, b1, b2, rng, t, prim);
   }
   for (;;) {
-    rt_object x = S.objects[target];
+    rt_object x = ro<F>(S.objects)[target];
     Ray rr = r;
     if constexpr ((F & F_XFORM) != 0) if (x.kind == RT_OBJ_XFORM) {
         Ray moved;
         rr = xform_ray(x, r, moved);
-        x = S.objects[x.a];
+        x = ro<F>(S.objects)[x.a];
     }
     float tq;
     int pq;
@@ -1324,7 +1349,7 @@ __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray&
     // the medium's record again (an opaque index: not kept live in VGPRs across the leaf query)
     int oi2 = oi;
     asm volatile("" : "+v"(oi2));
-    const rt_object o2 = S.objects[oi2];
+    const rt_object o2 = ro<F>(S.objects)[oi2];
     if (phase == 1) return medium_hit<F>(o2, r, tmin, tmax, t1, tq, rng, t, prim);
     t1 = tq;
     if (sphere_boundary_no_hit<F>(S, o2.a, t1)) return false;
@@ -1335,7 +1360,7 @@ __device__ __forceinline__ bool object_query(const DScene& S, int oi, const Ray&
 
 template <int F>
 __device__ __forceinline__ void object_record(const DScene& S, int oi, int prim, const Ray& r, float tmin, float t, Hit& h) {
-  const rt_object o = S.objects[oi];
+  const rt_object o = ro<F>(S.objects)[oi];
   if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {
       Ray moved;
       const Ray rr = xform_ray(o, r, moved);
@@ -1377,7 +1402,7 @@ __device__ __forceinline__ bool world_hit(const DScene& S, const Ray& r, Hit& h,
     if (w < 32 && ((mask >> w) & 1u) == 0) continue;
     float t;
     int pr;
-    const int oi = S.world[w];
+    const int oi = ro<F>(S.world)[w];
     if (object_query<F>(S, oi, r, 0.001f, closest, t, pr, rng, nnode, nprim, nfall)) {
       closest = t;
       wobj = oi;
@@ -1409,16 +1434,16 @@ __device__ __forceinline__ int world_search(const DScene& S, const Ray& r, uint3
   const int NW = S.n_world;
   for (int w = 0; w < NW; ++w) {
     if (w < 32 && ((mask >> w) & 1u) == 0) continue;
-    const rt_object o = S.objects[S.world[w]];
+    const rt_object o = ro<F>(S.objects)[ro<F>(S.world)[w]];
     if ((F & F_MEDIUM) != 0 && o.kind == RT_OBJ_MEDIUM) continue;  // inert (merge_ok), the ray is sane
     Ray rr = r;
-    int xi = S.world[w];
+    int xi = ro<F>(S.world)[w];
     if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {
       Ray moved;
       rr = xform_ray(o, r, moved);
       xi = o.a;
     }
-    const rt_object x = S.objects[xi];
+    const rt_object x = ro<F>(S.objects)[xi];
     const int kbase = (NW - 1 - w) << RT_WKEY_SHIFT;
     const float a = len2(rr.d), rcpa = __builtin_amdgcn_rcpf(a);
     if ((F & F_BVH) != 0 && x.kind == RT_OBJ_BVH) {
@@ -1442,9 +1467,9 @@ __device__ __forceinline__ int world_search(const DScene& S, const Ray& r, uint3
   }
   if (overflow || (best_prim >= 0 && !(second > bhi))) return 2;
   if (best_prim < 0) return 0;
-  wobj = S.world[NW - 1 - (best_key >> RT_WKEY_SHIFT)];
+  wobj = ro<F>(S.world)[NW - 1 - (best_key >> RT_WKEY_SHIFT)];
   prim = best_prim;
-  const rt_object o = S.objects[wobj];
+  const rt_object o = ro<F>(S.objects)[wobj];
   Ray rr = r;
   int xi = wobj;
   if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {
@@ -1458,7 +1483,7 @@ __device__ __forceinline__ int world_search(const DScene& S, const Ray& r, uint3
     if (!prim_t<F>(S, best_prim, rr, tmin, inf, best, np)) return 2;
   }
   if constexpr ((F & F_BVH) != 0) {
-    const rt_object x = S.objects[xi];
+    const rt_object x = ro<F>(S.objects)[xi];
     if (x.kind == RT_OBJ_BVH) {
       const float lim = __builtin_fminf(second, bhi * 1.0009765625f);
       if (!chain_ok<F>(S, x.a, x.b, rr, tmin, lim, best, best_prim, best_key & ((1 << RT_WKEY_SHIFT) - 1), nnode))
@@ -1485,8 +1510,8 @@ __device__ __forceinline__ bool world_query_merged(const DScene& S, const Ray& r
     bool hit = false;
     for (int w = 0; w < S.n_world; ++w) {
       if (w < 32 && ((mask >> w) & 1u) == 0) continue;
-      const int oi = S.world[w];
-      const rt_object o = S.objects[oi];
+      const int oi = ro<F>(S.world)[w];
+      const rt_object o = ro<F>(S.objects)[oi];
       const float tcl = hit ? best : __builtin_inff();
       float tq;
       int pq;
@@ -1501,7 +1526,7 @@ __device__ __forceinline__ bool world_query_merged(const DScene& S, const Ray& r
           rr = xform_ray(o, r, moved);
           xi = o.a;
         }
-        const rt_object x = S.objects[xi];
+        const rt_object x = ro<F>(S.objects)[xi];
         if ((F & F_BVH) != 0 && x.kind == RT_OBJ_BVH) {
           hq = bvh_exact<F>(S, x.a, x.b, rr, mk(1.0f / rr.d.x, 1.0f / rr.d.y, 1.0f / rr.d.z), tmin, tcl, tq, pq, nnode,
                             nprim, nfall);
@@ -2116,7 +2141,7 @@ void render_step_kernel(const RenderParams P) {
   __syncthreads();
   RT_STAMP(0);
 #endif
-  const rt_object obj = S.objects[S.world[0]];
+  const rt_object obj = ro<F>(S.objects)[ro<F>(S.world)[0]];
   const int tbase = (F & F_WORLD) != 0 ? S.wt_fb : obj.c;  // traversal tree of the world's BVH / the world tree
   const float tmin = 0.001f, tmax = __builtin_inff();  // render.h:63
   long long item = -1;  // -1: no item
@@ -2214,8 +2239,8 @@ void render_step_kernel(const RenderParams P) {
           hit = st == 1;
           // exact: every entry in list order (the reference's visit sets); else the media after the tree
           for (int w = exact ? 0 : S.w_media; w < S.n_world; ++w) {
-            const int oi = S.world[w];
-            const rt_object o = S.objects[oi];
+            const int oi = ro<F>(S.world)[w];
+            const rt_object o = ro<F>(S.objects)[oi];
             float tq;
             int pq;
             bool hq;
@@ -2230,7 +2255,7 @@ void render_step_kernel(const RenderParams P) {
                 rr = xform_ray(o, ray, moved);
                 xi = o.a;
               }
-              const rt_object x = S.objects[xi];
+              const rt_object x = ro<F>(S.objects)[xi];
               if ((F & F_BVH) != 0 && x.kind == RT_OBJ_BVH) {
                 hq = bvh_exact<F>(S, x.a, x.b, rr, mk(1.0f / rr.d.x, 1.0f / rr.d.y, 1.0f / rr.d.z), tmin, tcl, tq, pq,
                                   nnode, nprim, nfall);
@@ -2253,7 +2278,7 @@ void render_step_kernel(const RenderParams P) {
           // primitive objects after the BVH in the world list (C4's ground sphere): hittable_list's
           // rule, t_max = the closest hit so far (inclusive), so a later entry wins a tie
           for (int w = 1; w < S.n_world; ++w) {
-            const rt_object po = S.objects[S.world[w]];
+            const rt_object po = ro<F>(S.objects)[ro<F>(S.world)[w]];
             float tq;
             if (prim_t<F>(S, po.a, ray, tmin, hit ? best : tmax, tq, nprim)) {
               hit = true;
