@@ -381,6 +381,13 @@ __device__ __forceinline__ PrimRec load_prim(const DScene& S, int i) {
     return PrimRec{q[0], q[1], q[2]};
   }
 }
+// A wave-uniform primitive index in any global-memory variant: the record through ro (s_load).
+template <int F>
+__device__ __forceinline__ PrimRec load_prim_u(const DScene& S, int i) {
+  if constexpr ((F & F_LDS) != 0) return load_prim<F>(S, i);
+  const auto q = ro<0>(S.prims) + 3 * i;
+  return PrimRec{q[0], q[1], q[2]};
+}
 __device__ __forceinline__ int prim_type(const PrimRec& q) { return __float_as_int(q.c.z) & RT_PRIM_TYPE_MASK; }
 
 __device__ __forceinline__ bool sphere_t(const Ray& r, V c, float rad, float tmin, float tmax, float& t) {
@@ -1434,16 +1441,16 @@ __device__ __forceinline__ int world_search(const DScene& S, const Ray& r, uint3
   const int NW = S.n_world;
   for (int w = 0; w < NW; ++w) {
     if (w < 32 && ((mask >> w) & 1u) == 0) continue;
-    const rt_object o = ro<F>(S.objects)[ro<F>(S.world)[w]];
+    const rt_object o = ro<0>(S.objects)[ro<0>(S.world)[w]];
     if ((F & F_MEDIUM) != 0 && o.kind == RT_OBJ_MEDIUM) continue;  // inert (merge_ok), the ray is sane
     Ray rr = r;
-    int xi = ro<F>(S.world)[w];
+    int xi = ro<0>(S.world)[w];
     if constexpr ((F & F_XFORM) != 0) if (o.kind == RT_OBJ_XFORM) {
       Ray moved;
       rr = xform_ray(o, r, moved);
       xi = o.a;
     }
-    const rt_object x = ro<F>(S.objects)[xi];
+    const rt_object x = ro<0>(S.objects)[xi];
     const int kbase = (NW - 1 - w) << RT_WKEY_SHIFT;
     const float a = len2(rr.d), rcpa = __builtin_amdgcn_rcpf(a);
     if ((F & F_BVH) != 0 && x.kind == RT_OBJ_BVH) {
@@ -1459,7 +1466,7 @@ __device__ __forceinline__ int world_search(const DScene& S, const Ray& r, uint3
           break;
       }
     } else {
-      const PrimRec q = load_prim<F>(S, x.a);
+      const PrimRec q = load_prim_u<F>(S, x.a);
       float lo, hi;
       if (prim_range<F>(S, q, rr, a, rcpa, tmin, inf, lo, hi, nprim))
         take_candidate<true>(lo, hi, x.a, kbase, blo, bhi, second, best_prim, best_key);
@@ -2278,9 +2285,9 @@ void render_step_kernel(const RenderParams P) {
           // primitive objects after the BVH in the world list (C4's ground sphere): hittable_list's
           // rule, t_max = the closest hit so far (inclusive), so a later entry wins a tie
           for (int w = 1; w < S.n_world; ++w) {
-            const rt_object po = ro<F>(S.objects)[ro<F>(S.world)[w]];
+            const rt_object po = ro<0>(S.objects)[ro<0>(S.world)[w]];  // uniform: scalar loads
             float tq;
-            if (prim_t<F>(S, po.a, ray, tmin, hit ? best : tmax, tq, nprim)) {
+            if (prim_t_q<F>(S, load_prim_u<F>(S, po.a), ray, tmin, hit ? best : tmax, tq, nprim)) {
               hit = true;
               best = tq;
               best_prim = po.a;
