@@ -3212,7 +3212,7 @@ struct SahBuilder {
 };
 
 int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<rt_prim>& prims,
-                         std::vector<rt_bvh_node>& nodes, std::vector<float2>& pmargin) {
+                         std::vector<rt_bvh_node>& nodes, std::vector<float2>& pmargin, int* n_pairs) {
   const int inner = (1 << rows) - 1, last0 = (1 << (rows - 1)) - 1;
   std::vector<int> members;
   for (int k = last0; k < inner; ++k) {
@@ -3284,6 +3284,7 @@ int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<
   nodes.resize(fb + 2);  // record 0 = root
   SahBuilder sb{box, nodes, fb};
   sb.build(leaves.data(), (int)leaves.size(), 0);
+  *n_pairs = (int)leaves.size() - 1;  // records of the tree (one per inner node): leaves - 1
   return fb;
 }
 
@@ -3875,11 +3876,13 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   std::vector<rt_bvh_node> nodes(s->nodes, s->nodes + s->n_nodes);
   std::vector<rt_object> objects(s->objects, s->objects + s->n_objects);
   std::vector<float2> pmargin(s->n_prims, make_float2(-INFINITY, -INFINITY));
-  for (rt_object& o : objects) {
+  std::vector<int> tree_pairs(objects.size(), 0);  // records of each BVH object's traversal tree
+  for (size_t k = 0; k < objects.size(); ++k) {
+    rt_object& o = objects[k];
     o.c = -1;
     if (o.kind == RT_OBJ_MEDIUM && medium_inert(s, o)) o.c = 1;  // object_query skips it for sane rays
     if (o.kind == RT_OBJ_BVH) {
-      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes, pmargin);
+      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes, pmargin, &tree_pairs[k]);
       if (fast < 0) return fail(c, RT_ERR_SCENE, "malformed reference bvh");
       o.c = fast;
     }
@@ -3910,13 +3913,12 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   std::vector<uint32_t> qnodes;
   int q_pairs = 0, q_ebias = 0;
   if (world_step && !getenv("RT_NO_QLDS")) {  // the world BVH's traversal tree, quantized (F_QLDS)
+    // (the tree's own record count: coincident triangles are not leaves of it)
     const rt_object& wo = objects[(size_t)s->world[0]];
-    int n = 0;
-    const int inner = (1 << wo.b) - 1, last0 = (1 << (wo.b - 1)) - 1;
-    for (int k = last0; k < inner; ++k) n += (s->nodes[wo.a + k].leaf_a >= 0) + (s->nodes[wo.a + k].leaf_b >= 0);
-    if (n >= 2 && (size_t)(n - 1) * 24 + 1024 * kStackDepth * 2 <= (size_t)kLdsBudget &&
-        build_qtree(nodes, wo.c, n - 1, qnodes, q_ebias))
-      q_pairs = n - 1;
+    const int np = tree_pairs[(size_t)s->world[0]];
+    if (np >= 1 && (size_t)np * 24 + 1024 * kStackDepth * 2 <= (size_t)kLdsBudget &&
+        build_qtree(nodes, wo.c, np, qnodes, q_ebias))
+      q_pairs = np;
   }
   DScene& d = c->scene;
   d = DScene{};

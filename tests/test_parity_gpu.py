@@ -321,6 +321,13 @@ def test_coincident_triangles_leave_the_traversal_tree(rtlib, gpu_ctx, monkeypat
         assert out[mode][1]["segments"] == out["dedup"][1]["segments"]
         assert np.array_equal(_bits(out[mode][0]), _bits(out["dedup"][0])), mode
     assert out["dedup"][1]["prim_tests"] < out["all"][1]["prim_tests"]
+    if scene == "door":  # the product variant keeps the (smaller) tree quantized in LDS (F_QLDS = 1 << 16)
+        fb = torch.zeros(nfb * H * W * 3, dtype=torch.float32, device="cuda")
+        cnt = gpu_ctx.render(rtlib.make_args(W, H, spp, 0, nfb, 50, REF), fb.data_ptr())
+        name = gpu_ctx.last_render_kernel()
+        assert name.startswith("render_step_kernel<") and int(name.split("<")[1].split(">")[0]) & (1 << 16), name
+        assert cnt["segments"] == out["dedup"][1]["segments"]
+        assert np.array_equal(_bits(fb.cpu().numpy()), _bits(out["dedup"][0]))
 
 
 @pytest.mark.parametrize("scene,W,H,spp,nfb,cam", [
