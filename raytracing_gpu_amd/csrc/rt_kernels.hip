@@ -1839,13 +1839,16 @@ constexpr int render_wpe() {
 #ifndef RT_WPE_FINAL
 #define RT_WPE_FINAL 4
 #endif
+#ifndef RT_WPE_CORNELL
+#define RT_WPE_CORNELL 4
+#endif
 #ifndef RT_WPE_MESH
 #define RT_WPE_MESH 4
 #endif
   return (F & F_LDS) != 0 ? 1
                           : (feat == F_FINAL ? RT_WPE_FINAL
                                              : (feat == F_MESH ? RT_WPE_MESH
-                                                               : (feat == F_CORNELL ? 4 : (feat == F_ALL ? 3 : 1))));
+                                                               : (feat == F_CORNELL ? RT_WPE_CORNELL : (feat == F_ALL ? 3 : 1))));
 #endif
 }
 template <int F>
