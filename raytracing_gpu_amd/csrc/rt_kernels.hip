@@ -206,8 +206,17 @@ constexpr int kLockerSmall = 5;  // variants that park only the sample sum, fb a
 // scratch at the 4-wave floor.  C5 F_FINAL at 3840x2159 4x4 (MI355X): 86.0 ms with 200 B of
 // scratch per lane; 81.6 ms with words 5..14 parked (140 B); 80.7 ms with the RNG state too (132 B).
 // F_CORNELL (no spills) ran 1 % slower with words 5..14 parked, so it keeps the small locker.
+#ifndef RT_PARK_CORNELL
+#define RT_PARK_CORNELL 0
+#endif
 constexpr bool parks_segment_mask(int mask) {
-  return (mask & (F_LDS | F_STEP)) == 0 && ((mask & F_ALL) == F_FINAL || (mask & F_ALL) == F_ALL);
+  return (mask & (F_LDS | F_STEP)) == 0 &&
+         ((mask & F_ALL) == F_FINAL || (mask & F_ALL) == F_ALL || (RT_PARK_CORNELL && (mask & F_ALL) == F_CORNELL));
+}
+// LDS words per lane of traversal stack: render_kernel's global-memory variants without BVHs (C3's
+// list of rects and media) traverse nothing and keep none, so their locker starts at word 0.
+constexpr int stack_words(int mask) {
+  return (mask & (F_LDS | F_STEP | F_QLDS | F_BVH)) == 0 ? 0 : kStackDepth;
 }
 // render_step_kernel: the world-tree variants park their per-item / per-sample state in a locker
 // of kLockerStep words (step_parks_mask); the others keep none (only the traversal stack is in LDS).
@@ -229,7 +238,7 @@ constexpr bool parks() {
 }
 template <int F>
 __device__ __forceinline__ uint32_t* locker_of() {
-  return (uint32_t*)rt_lds + render_block<F>() * kStackDepth + threadIdx.x;
+  return (uint32_t*)rt_lds + render_block<F>() * stack_words(F) + threadIdx.x;
 }
 
 // Stage the read-only scene arrays a F_LDS variant reads in LDS, once per workgroup.
@@ -1840,7 +1849,7 @@ constexpr int render_wpe() {
 #define RT_WPE_FINAL 4
 #endif
 #ifndef RT_WPE_CORNELL
-#define RT_WPE_CORNELL 4
+#define RT_WPE_CORNELL 5
 #endif
 #ifndef RT_WPE_MESH
 #define RT_WPE_MESH 4
@@ -1913,7 +1922,7 @@ void render_kernel(const RenderParams P) {
   // the RNG state: parked too; the world query (media draws) uses it in place, the camera ray and
   // scatter on a register copy
   Rng loc_r{};
-  Rng& loc = cold_ref<PK>(loc_r, (uint32_t*)rt_lds + LB * (kStackDepth + 15) + 6 * threadIdx.x);
+  Rng& loc = cold_ref<PK>(loc_r, (uint32_t*)rt_lds + LB * (stack_words(F) + 15) + 6 * threadIdx.x);
   Ray ray{};
   V col = mk(0, 0, 0);
   unsigned nnode = 0, nprim = 0, nfall = 0;
@@ -3516,7 +3525,7 @@ int rt_ctx_create(int hip_device, rt_ctx** out) {
     for (int v = 0; v < kNumVariants; ++v)
       chk(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c->blocks_per_cu[v], kVariants[v].fn, variant_block(v),
                                                        (kVariants[v].mask & (F_LDS | F_QLDS)) ? kLdsBudget
-                                                                                   : variant_block(v) * (kStackDepth + locker_words(kVariants[v].mask)) * 4),
+                                                                                   : variant_block(v) * (stack_words(kVariants[v].mask) + locker_words(kVariants[v].mask)) * 4),
           "occupancy");
   }
   if (rc != RT_OK) {
@@ -4312,7 +4321,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   const bool qlds_var = (kVariants[var].mask & F_QLDS) != 0;
   const size_t shmem = lds_var    ? lds_bytes + (size_t)bs * kStackDepth * 2
                        : qlds_var ? (size_t)c->scene.q_pairs * 24 + (size_t)bs * kStackDepth * 2
-                                  : (size_t)bs * (kStackDepth + locker_words(kVariants[var].mask)) * 4;
+                                  : (size_t)bs * (stack_words(kVariants[var].mask) + locker_words(kVariants[var].mask)) * 4;
   // Camera-ray culling, built once per (scene, W, H): candidate lists for the stepwise kernel
   // (world = one BVH), top-level entry masks for list worlds.  Not in the exact / audit modes,
   // whose counters are the reference's.
