@@ -4,4 +4,4 @@ crash() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
 timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/t_all.log 2>&1; rc=$?
 grep -E "FAIL|ERROR|passed|failed" gpurun_out/t_all.log | tail -20; echo all rc=$rc; crash $rc && exit $rc
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; echo smoke rc=$?; tail -1 gpurun_out/smoke.log
-bash scripts/final_r04.sh
+bash scripts/r04/final_r04.sh
