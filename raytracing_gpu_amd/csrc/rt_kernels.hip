@@ -96,6 +96,7 @@ struct DScene {
   int32_t lds_prims;     // F_LDS: primitive count staged (validation margins follow them)
   int32_t lds_mats;      // F_LDS: materials staged after the margins (one float4 each)
   int32_t lds_texs;      // F_LDS: textures staged after the materials (two float4 each; stacks follow)
+  int32_t lds_imgs;      // F_QLDS: images staged after the textures (one float4 each)
   const float4* cam_tab; // REF camera mode: lens offset (xyz) and time (w) of sample s (camera_ray)
   // F_WORLD (list world as one traversal tree, see build_world_tree): 4 float4 per leaf -- the
   // primitive's record (c.y = tie key, RT_PRIM_FLAG_XF in the type word for instance members) and
@@ -164,20 +165,35 @@ __device__ __forceinline__ const float2* pmargin_of(const DScene& S) {
   if constexpr ((F & F_LDS) != 0) return (const float2*)(rt_lds + 2 * S.lds_nodes + 3 * S.lds_prims);
   else return S.pmargin;
 }
-static_assert(sizeof(rt_material) == 16 && sizeof(rt_texture) == 32, "LDS staging copies whole float4s");
+static_assert(sizeof(rt_material) == 16 && sizeof(rt_texture) == 32 && sizeof(rt_image) == 16,
+              "LDS staging copies whole float4s");
+constexpr int kStackDepthQ = 16;  // = kStackDepth (the F_QLDS stacks, 16-bit entries)
 // Materials and textures (F_LDS: staged after the margins; read once per segment by scatter).
 __device__ __forceinline__ int lds_mats_at(const DScene& S) {
   return 2 * S.lds_nodes + 3 * S.lds_prims + (S.lds_prims + 1) / 2;
 }
+// F_QLDS: materials, textures and images staged after the quantized tree and its 16-bit stacks (one,
+// two and one float4 each), so the shading phase's dependent chain (material -> texture -> image ->
+// texel) reads LDS instead of L2 until the texel itself.
+__host__ __device__ __forceinline__ int qlds_mats_at(const DScene& S) {
+  return ((6 * S.q_pairs + 1024 * kStackDepthQ / 2) + 3) / 4;  // float4 index, 16-byte aligned
+}
 template <int F>
 __device__ __forceinline__ const int4* mats_of(const DScene& S) {
   if constexpr ((F & F_LDS) != 0) return (const int4*)(rt_lds + lds_mats_at(S));
+  else if constexpr ((F & F_QLDS) != 0) return (const int4*)(rt_lds + qlds_mats_at(S));
   else return S.mats;
 }
 template <int F>
 __device__ __forceinline__ const rt_texture* texs_of(const DScene& S) {
   if constexpr ((F & F_LDS) != 0) return (const rt_texture*)(rt_lds + lds_mats_at(S) + S.lds_mats);
+  else if constexpr ((F & F_QLDS) != 0) return (const rt_texture*)(rt_lds + qlds_mats_at(S) + S.lds_mats);
   else return S.texs;
+}
+template <int F>
+__device__ __forceinline__ const rt_image* imgs_of(const DScene& S) {
+  if constexpr ((F & F_QLDS) != 0) return (const rt_image*)(rt_lds + qlds_mats_at(S) + S.lds_mats + 2 * S.lds_texs);
+  else return S.images;
 }
 // Stack entries: child words (pair index, or -1 - primitive).  F_LDS scenes have < 32768 pairs and
 // primitives (they fit in LDS), so their entries are 16-bit (32 KB of stacks per 1024 lanes).
@@ -1610,7 +1626,7 @@ __device__ __forceinline__ V tex_leaf(const DScene& S, const rt_texture& T, floa
   }
   if constexpr ((F & F_IMAGE) != 0) {
     if (T.type == RT_TEX_IMAGE) {  // texture.h:145-163
-      const rt_image im = S.images[T.a];
+      const rt_image im = imgs_of<F>(S)[T.a];
       if (im.width <= 0) return mk(0.0f, 1.0f, 1.0f);
       const float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
       const float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
@@ -2151,6 +2167,12 @@ void render_step_kernel(const RenderParams P) {
   if constexpr ((F & F_QLDS) != 0) {  // the quantized traversal tree (24-byte pair records)
     uint32_t* q = (uint32_t*)rt_lds;
     for (int k = threadIdx.x; k < 6 * S.q_pairs; k += render_block<F>()) q[k] = S.qnodes[k];
+    // ... and after its stacks the materials, textures and images (lds_mats / lds_texs / lds_imgs)
+    float4* m = rt_lds + qlds_mats_at(S);
+    const int nm = S.lds_mats, nt = 2 * S.lds_texs, ni = S.lds_imgs;
+    for (int k = threadIdx.x; k < nm + nt + ni; k += render_block<F>())
+      m[k] = k < nm ? ((const float4*)S.mats)[k]
+                    : (k < nm + nt ? ((const float4*)S.texs)[k - nm] : ((const float4*)S.images)[k - nm - nt]);
     __syncthreads();
   }
   const unsigned lane = __lane_id();
@@ -2971,7 +2993,7 @@ struct rt_ctx {
   bool world_bvh = false;  // the world list is one BVH object (camera tile lists apply)
   bool world_step = false;  // one BVH object followed by primitive objects (render_step_kernel applies)
   bool world_tree = false;  // a list world flattened into the world tree (render_step_kernel<..|F_WORLD>)
-  int dev_nodes = 0, dev_prims = 0, dev_mats = 0, dev_texs = 0;  // device array sizes (for LDS staging)
+  int dev_nodes = 0, dev_prims = 0, dev_mats = 0, dev_texs = 0, dev_imgs = 0;  // device array sizes (LDS staging)
   float last_ms = 0.0f;
   int last_sched = 0;  // RT_SCHED_* of the last render launch
   char last_kernel[48] = "";  // rocprof name stem of the last render launch, e.g. render_step_kernel<25730>
@@ -3930,7 +3952,8 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
     // (the tree's own record count: coincident triangles are not leaves of it)
     const rt_object& wo = objects[(size_t)s->world[0]];
     const int np = tree_pairs[(size_t)s->world[0]];
-    if (np >= 1 && (size_t)np * 24 + 1024 * kStackDepth * 2 <= (size_t)kLdsBudget &&
+    const size_t tables = 16 * ((size_t)s->n_materials + 2 * (size_t)s->n_textures + (size_t)s->n_images) + 16;
+    if (np >= 1 && (size_t)np * 24 + 1024 * kStackDepth * 2 + tables <= (size_t)kLdsBudget &&
         build_qtree(nodes, wo.c, np, qnodes, q_ebias))
       q_pairs = np;
   }
@@ -4061,6 +4084,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   c->dev_nodes = (int)nodes.size();
   c->dev_prims = (int)prims.size();
   c->dev_mats = s->n_materials;
+  c->dev_imgs = s->n_images;
   c->dev_texs = s->n_textures;
   c->have_scene = true;
   return RT_OK;
@@ -4363,11 +4387,13 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   const bool lds_var = (kVariants[var].mask & F_LDS) != 0;
   P.S.lds_nodes = lds_var ? c->dev_nodes : 0;
   P.S.lds_prims = lds_var ? c->dev_prims : 0;
-  P.S.lds_mats = lds_var ? c->dev_mats : 0;
-  P.S.lds_texs = lds_var ? c->dev_texs : 0;
   const bool qlds_var = (kVariants[var].mask & F_QLDS) != 0;
+  P.S.lds_mats = (lds_var || qlds_var) ? c->dev_mats : 0;
+  P.S.lds_texs = (lds_var || qlds_var) ? c->dev_texs : 0;
+  P.S.lds_imgs = qlds_var ? c->dev_imgs : 0;
+  static_assert(kStackDepthQ == kStackDepth, "F_QLDS stacks");
   const size_t shmem = lds_var    ? lds_bytes + (size_t)bs * kStackDepth * 2
-                       : qlds_var ? (size_t)c->scene.q_pairs * 24 + (size_t)bs * kStackDepth * 2
+                       : qlds_var ? (size_t)16 * (qlds_mats_at(P.S) + c->dev_mats + 2 * c->dev_texs + c->dev_imgs)
                                   : (size_t)bs * (stack_words(kVariants[var].mask) + locker_words(kVariants[var].mask)) * 4;
   // Camera-ray culling, built once per (scene, W, H): candidate lists for the stepwise kernel
   // (world = one BVH), top-level entry masks for list worlds.  Not in the exact / audit modes,
