@@ -178,16 +178,29 @@ __device__ __forceinline__ int lds_mats_at(const DScene& S) {
 __host__ __device__ __forceinline__ int qlds_mats_at(const DScene& S) {
   return ((6 * S.q_pairs + 1024 * kStackDepthQ / 2) + 3) / 4;  // float4 index, 16-byte aligned
 }
+// render_kernel's variants without BVHs or triangles (C3) stage them after their locker too.
+constexpr int stack_words(int mask);
+constexpr int locker_words(int mask);
+template <int F>
+constexpr bool tables_after_locker() {
+  return (F & (F_LDS | F_QLDS | F_STEP | F_BVH | F_TRI)) == 0;
+}
+template <int F>
+constexpr int locker_tables_at() {  // float4 index after the stacks and the locker (256-thread blocks)
+  return 256 * (stack_words(F) + locker_words(F)) / 4;
+}
 template <int F>
 __device__ __forceinline__ const int4* mats_of(const DScene& S) {
   if constexpr ((F & F_LDS) != 0) return (const int4*)(rt_lds + lds_mats_at(S));
   else if constexpr ((F & F_QLDS) != 0) return (const int4*)(rt_lds + qlds_mats_at(S));
+  else if constexpr (tables_after_locker<F>()) return (const int4*)(rt_lds + locker_tables_at<F>());
   else return S.mats;
 }
 template <int F>
 __device__ __forceinline__ const rt_texture* texs_of(const DScene& S) {
   if constexpr ((F & F_LDS) != 0) return (const rt_texture*)(rt_lds + lds_mats_at(S) + S.lds_mats);
   else if constexpr ((F & F_QLDS) != 0) return (const rt_texture*)(rt_lds + qlds_mats_at(S) + S.lds_mats);
+  else if constexpr (tables_after_locker<F>()) return (const rt_texture*)(rt_lds + locker_tables_at<F>() + S.lds_mats);
   else return S.texs;
 }
 template <int F>
@@ -1883,6 +1896,13 @@ __global__ __launch_bounds__(render_block<F>()) __attribute__((amdgpu_waves_per_
 void render_kernel(const RenderParams P) {
   const DScene& S = P.S;
   if constexpr ((F & F_LDS) != 0) stage_lds<F>(S);  // nodes, primitives, margins, materials, textures
+  if constexpr (tables_after_locker<F>()) {  // materials and textures after the locker
+    static_assert(render_block<F>() == 256, "locker_tables_at assumes 256-thread blocks");
+    float4* m = rt_lds + locker_tables_at<F>();
+    const int nm = S.lds_mats, nt = 2 * S.lds_texs;
+    for (int k = threadIdx.x; k < nm + nt; k += 256) m[k] = k < nm ? ((const float4*)S.mats)[k] : ((const float4*)S.texs)[k - nm];
+    __syncthreads();
+  }
   const unsigned lane = __lane_id();
 #ifdef RT_STEP_DIAG
   if (lane < 4) rt_diag_acc[threadIdx.x >> 6][lane] = 0;
@@ -4272,8 +4292,14 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
                        c->dev_prims < 32768 && (a->flags & RT_FLAG_NO_LDS) == 0;
   const bool step = (c->world_step || c->world_tree) && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
   const bool qlds = !use_lds && c->scene.q_pairs > 0 && (a->flags & RT_FLAG_NO_LDS) == 0;
-  const int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
-                               (a->flags & RT_FLAG_WIDEST) != 0, step, c->world_tree, qlds, c->scene.merge_ok != 0);
+  // the variants that stage their materials and textures after the locker (tables_after_locker) need
+  // them to fit: a list world without BVHs whose tables exceed 32 KB runs the widest variant instead
+  const bool big_tables = (size_t)16 * ((size_t)c->dev_mats + 2 * (size_t)c->dev_texs) > 32768;
+  int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
+                         (a->flags & RT_FLAG_WIDEST) != 0, step, c->world_tree, qlds, c->scene.merge_ok != 0);
+  if (var >= 0 && big_tables && (kVariants[var].mask & (F_LDS | F_QLDS | F_STEP | F_BVH | F_TRI)) == 0)
+    var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds, true, step,
+                       c->world_tree, qlds, c->scene.merge_ok != 0);
   if (var < 0) return fail(c, RT_ERR_SCENE, "no kernel variant covers the scene features");
   // shading phase of render_step_kernel once this many lanes of a wave wait (RT_SHADE_MIN: tuning)
   // (measured: C2 best at 60 of 64 lanes; C4's triangle-mesh steps at 48: 125.0 -> 119.7 ms, 40: 121.8)
@@ -4388,13 +4414,16 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   P.S.lds_nodes = lds_var ? c->dev_nodes : 0;
   P.S.lds_prims = lds_var ? c->dev_prims : 0;
   const bool qlds_var = (kVariants[var].mask & F_QLDS) != 0;
-  P.S.lds_mats = (lds_var || qlds_var) ? c->dev_mats : 0;
-  P.S.lds_texs = (lds_var || qlds_var) ? c->dev_texs : 0;
+  const int vmask = kVariants[var].mask;
+  const bool tables_var = (vmask & (F_LDS | F_QLDS | F_STEP | F_BVH | F_TRI)) == 0;
+  P.S.lds_mats = (lds_var || qlds_var || tables_var) ? c->dev_mats : 0;
+  P.S.lds_texs = (lds_var || qlds_var || tables_var) ? c->dev_texs : 0;
   P.S.lds_imgs = qlds_var ? c->dev_imgs : 0;
   static_assert(kStackDepthQ == kStackDepth, "F_QLDS stacks");
   const size_t shmem = lds_var    ? lds_bytes + (size_t)bs * kStackDepth * 2
                        : qlds_var ? (size_t)16 * (qlds_mats_at(P.S) + c->dev_mats + 2 * c->dev_texs + c->dev_imgs)
-                                  : (size_t)bs * (stack_words(kVariants[var].mask) + locker_words(kVariants[var].mask)) * 4;
+                                  : (size_t)bs * (stack_words(vmask) + locker_words(vmask)) * 4 +
+                                        (tables_var ? (size_t)16 * (c->dev_mats + 2 * c->dev_texs) : 0);
   // Camera-ray culling, built once per (scene, W, H): candidate lists for the stepwise kernel
   // (world = one BVH), top-level entry masks for list worlds.  Not in the exact / audit modes,
   // whose counters are the reference's.
