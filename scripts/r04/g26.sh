@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-4: C4's quantized-tree variant with materials, textures and images staged in LDS
-# (build/ab/libtables.so, scripts/r04/qlds_tables.patch on the final round-4 source): GPU suite on
+# (build/ab/libtables.so: this change on the final round-4 source, committed after the run): GPU suite on
 # that library, then same-box A/B against the tree's kernels
 export TMPDIR=/tmp; mkdir -p gpurun_out
 RT_HIP_LIB=build/ab/libtables.so timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/t_tables.log 2>&1; rc=$?

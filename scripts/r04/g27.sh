@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-4: C3's variant with materials and textures staged in LDS after its locker
-# (build/ab/libc3tables.so = scripts/r04/c3_tables.patch on the final source): GPU suite on that
+# (build/ab/libc3tables.so: this change on the final source, committed after the run): GPU suite on that
 # library, then same-box A/B against the tree's kernels
 export TMPDIR=/tmp; mkdir -p gpurun_out
 RT_HIP_LIB=build/ab/libc3tables.so timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/t_c3tables.log 2>&1; rc=$?
