@@ -101,12 +101,24 @@ def parse():
     ap.add_argument("--cold-steps", type=int, default=3, help="draws timed with nothing reused (cold_ms_per_step)")
     ap.add_argument("--gather", default="rccl", choices=["rccl", "host"],
                     help="--gpus N without a launcher: ncclGather over distinct devices, or host copies (ranks may share a GPU)")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="context option (include/rt_hip.h rt_ctx_options), e.g. --opt shade_min=52; "
+                         "one-process-per-GPU path only")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="debug: gloo runs the N>1 path with host-side collectives and ranks sharing the visible GPUs")
     a = ap.parse_args()
     if a.steps < 1 or a.warmup < 0 or a.cold_steps < 0 or a.gpus < 1:
         ap.error("--steps and --gpus must be >= 1, --warmup and --cold-steps >= 0")
     return a
+
+
+def parse_opts(items) -> dict:
+    """--opt KEY=VALUE pairs -> rt_ctx_options fields (ints, or floats where the field is a float)."""
+    out = {}
+    for it in items:
+        k, _, v = it.partition("=")
+        out[k.strip()] = float(v) if any(ch in v for ch in ".e") else int(v)
+    return out
 
 
 CONFIG_OF = {"big1": "C2", "random": "C2", "cornell_smoke": "C3", "door": "C4", "final": "C5"}
@@ -268,6 +280,9 @@ def main():
     cdev = torch.device("cpu") if a.backend == "gloo" else dev  # where collectives run
 
     ctx = rt.Context(local)
+    opts = parse_opts(a.opt)
+    if opts:
+        ctx.set_options(**opts)
     sc = rt.Scene.builtin(a.scene, **scene_assets(a.scene)[0])
     ctx.upload(sc)
     cam = rt.RT_CAM_REF_SLOT0 if a.cam == "ref" else rt.RT_CAM_PER_PIXEL
@@ -358,6 +373,7 @@ def main():
         roof = roofline(a, stats, kname[0], avg_ms, len(rows), workload, world)
         extra = {"cold_ms_per_step": round(dt_cold * 1e3, 3), "cold_value": round(segs / dt_cold / 1e6, 2),
                  "cold_kernel_ms": round(cold_kms, 3), "kernel_ms": round(avg_ms, 3),
+                 "context_options": opts or "defaults",
                  "schedule": "steady state: every timed draw repeats the configuration and reuses the item "
                              "schedule (and split-sample states) of the draws before it; cold_* = draws that "
                              "reuse nothing (RT_FLAG_NO_SCHEDULE), as a single draw() runs",

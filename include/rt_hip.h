@@ -208,6 +208,52 @@ typedef struct rt_ctx rt_ctx;
 int rt_ctx_create(int hip_device, rt_ctx** out);
 int rt_ctx_destroy(rt_ctx* ctx);
 const char* rt_last_error(const rt_ctx* ctx);
+
+/* Implementation options of a context.  None of them changes a pixel or a segment count (every
+ * setting is parity-tested against the oracle); they choose kernel variants, search algorithms and
+ * schedule thresholds.  rt_ctx_options_default gives the measured product configuration, which a new
+ * context starts with; the library reads no environment variable.  The upload-time fields apply from
+ * the next rt_scene_upload; rt_ctx_set_options also drops the context's item schedule, so the next
+ * launch of any configuration is a cold one. */
+enum rt_merge_mode {
+  RT_MERGE_ON = 0,           /* list worlds of primitives, BVHs, instances and inert media: one
+                                candidate search over every entry (world_search)                 */
+  RT_MERGE_OFF = 1,          /* the per-entry list loop of hittable_list.h:23-39 (world_hit)     */
+  RT_MERGE_FALLBACK_ALL = 2  /* testing: run the search, then answer every query exactly         */
+};
+enum rt_merge_order {
+  RT_ORDER_DISTANCE = 0,     /* merged search visits primitives, then BVHs / instances nearest the
+                                camera first, then inert media                                    */
+  RT_ORDER_LIST = 1,         /* the list's own order                                               */
+  RT_ORDER_REVERSED = 2      /* testing: the list reversed                                         */
+};
+typedef struct rt_ctx_options {
+  /* upload time (rt_scene_upload) */
+  int32_t world_tree;        /* 1: a list world flattened into ONE traversal tree for the stepwise
+                                kernel (measured slower than the merged search; default 0)         */
+  int32_t quantized_tree;    /* 1: the world BVH's traversal tree as 24-byte records in LDS when it
+                                fits (C4's mesh; default 1)                                         */
+  int32_t merged_search;     /* rt_merge_mode (default RT_MERGE_ON)                                */
+  int32_t merge_order;       /* rt_merge_order (default RT_ORDER_DISTANCE)                         */
+  int32_t dedup_triangles;   /* 1: coincident triangles leave the traversal trees, the first of a
+                                group stands for it (default 1)                                     */
+  /* per launch (rt_render) */
+  int32_t shade_min;         /* stepwise kernel: lanes waiting before a wave shades; 0 = the
+                                variant's measured value (60, 56 for triangle meshes)               */
+  float bins_min_items_per_lane; /* camera-ray tile lists from this many items per resident lane
+                                (default 6; 0 = always)                                             */
+  float split_min_segments;  /* > 0: split the samples of items of at least this many segments;
+                                0 = the share-size rule (default)                                   */
+  int32_t split_order;       /* 1: split samples and unsplit items claimed in one longest-first
+                                sequence (default); 0: split samples first, in item order          */
+  int32_t cost_shift;        /* item-schedule cost buckets of 2^cost_shift segments; -1 = automatic */
+  float long_pct;            /* share of the longest items whose waves run at raised priority
+                                (default 2)                                                         */
+  int32_t pad;
+} rt_ctx_options;
+void rt_ctx_options_default(rt_ctx_options* opts);
+int rt_ctx_set_options(rt_ctx* ctx, const rt_ctx_options* opts);
+int rt_ctx_get_options(const rt_ctx* ctx, rt_ctx_options* opts);
 /* Rows of the image owned by a band tiling (ascending); returns the count. rows may be NULL. */
 int32_t rt_owned_rows(const rt_render_args* a, int32_t* rows);
 

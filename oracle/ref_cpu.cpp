@@ -1163,6 +1163,55 @@ static bool build_final(ref_scene& s, const ref_assets* a, Draw& g) {
   return true;
 }
 
+// Test scenes "coincident" / "coincident_step" (not in scenes.h; parity fixtures of the list and BVH
+// tie rules, the same compositions as rt_scene.cpp's scene_coincident).  "coincident": xy_rects lying
+// in the plane z = 0 in three kinds of list entries -- a primitive, members of a bvh_node and a
+// translate(rotate_y(.., 0)) instance (rotate_y by 0 and a translation in x, y leave the ray's z terms
+// exact) -- so world queries meet exact ties across entries (hittable_list.h:23-39: t_max = the
+// closest so far, inclusive, the later entry wins) and inside the BVH (bvh.h: strictly closer, the
+// first visited wins); the BVH also holds an xz_rect (H4 box), spheres and a rect behind the plane.
+// "coincident_step": a BVH, then primitives; a triangle repeated bit for bit inside the BVH and once
+// more after it (triangle.h's t depends on v0, e0, e1 only, so equal triangles tie exactly).
+static void build_coincident(ref_scene& s, Draw& g, bool step) {
+  s.background = kSky;
+  auto* red = s.lam(V3(0.8f, 0.1f, 0.1f));
+  auto* green = s.lam(V3(0.1f, 0.8f, 0.1f));
+  auto* yellow = s.lam(V3(0.8f, 0.8f, 0.1f));
+  auto* blue = s.lam(V3(0.1f, 0.2f, 0.8f));
+  auto* cyan = s.lam(V3(0.1f, 0.8f, 0.8f));
+  auto* grey = s.lam(V3(0.5f, 0.5f, 0.5f));
+  auto* metal = s.M<Metal>(s.X<Solid>(V3(0.8f, 0.8f, 0.8f)), 0.05f);
+  auto* glass = s.M<Dielectric>(1.5f);
+  const Hittable* ground = nullptr;
+  if (step) {
+    const float uv[6] = {0, 0, 1, 0, 0, 1};
+    const V3 a(-1.0f, -1.5f, 0.0f), b(2.0f, -1.5f, 0.0f), c(-1.0f, 0.5f, 0.0f), d(2.0f, 0.5f, 0.0f);
+    std::vector<const Hittable*> L = {
+        s.H<Triangle>(a, b, c, uv, nullptr, green), s.H<Triangle>(b, d, c, uv, nullptr, blue),
+        s.H<Sphere>(V3(2.2f, -0.3f, -0.8f), 0.5f, metal), s.H<Triangle>(a, b, c, uv, nullptr, yellow),
+        s.H<Sphere>(V3(-2.0f, 0.2f, -1.0f), 0.6f, glass)};
+    const Hittable* bvh = s.H<RefBvh>(L, 0.0f, 1.0f, g);
+    const Hittable* again = s.H<Triangle>(a, b, c, uv, nullptr, red);
+    ground = s.H<Sphere>(V3(0.0f, -101.7f, 0.0f), 100.0f, grey);
+    s.world = s.list({bvh, again, ground});
+  } else {
+    std::vector<const Hittable*> L = {
+        s.H<Rect>(2, -1.0f, 2.0f, -1.5f, 0.5f, 0.0f, green),
+        s.H<Rect>(2, -3.0f, 3.0f, 0.8f, 2.0f, 0.5f, blue),
+        s.H<Sphere>(V3(2.2f, -0.3f, -0.8f), 0.5f, metal),
+        s.H<Rect>(2, -0.5f, 0.7f, -1.2f, -0.2f, 0.0f, yellow),
+        s.H<Rect>(1, -3.0f, 3.0f, -3.0f, 3.0f, -1.6f, grey),
+        s.H<Sphere>(V3(-2.0f, 0.2f, -1.0f), 0.6f, glass)};
+    const Hittable* bvh = s.H<RefBvh>(L, 0.0f, 1.0f, g);
+    const Hittable* prim = s.H<Rect>(2, -2.0f, 0.5f, -1.0f, 1.0f, 0.0f, red);
+    ground = s.H<Sphere>(V3(0.0f, -101.7f, 0.0f), 100.0f, grey);
+    const Hittable* inst = s.H<Translate>(s.H<RotateY>(s.H<Rect>(2, -0.75f, 1.25f, -0.6f, 1.1f, 0.0f, cyan), 0.0f),
+                                          V3(0.25f, 0.1f, 0.0f));
+    s.world = s.list({prim, bvh, inst, ground});
+  }
+  s.cam = Camera(V3(0.3f, 0.4f, -6.0f), V3(0, 0, 0), V3(0, 1, 0), 40, 16.0f / 9.0f, 0.1f, 6.0f, 0, 1);
+}
+
 // ---------------------------------------------------------------- integrator (render.h:55-113)
 static V3 trace(const ref_scene& s, Ray r, Draw& g, int depth) {
   V3 att(1, 1, 1);
@@ -1237,6 +1286,8 @@ int ref_scene_create_ex(const char* name, int rtl, const ref_assets* a, ref_scen
   else if (n == "door") { if (!build_mesh_scene(*s, a, g, V3(-3, 4, -5), V3(0, 1, 0))) return 1; }
   else if (n == "cup") { if (!build_mesh_scene(*s, a, g, V3(0, 0, -1), V3(0, 0, 0))) return 1; }
   else if (n == "final") { if (!build_final(*s, a, g)) return 1; }
+  else if (n == "coincident") build_coincident(*s, g, false);
+  else if (n == "coincident_step") build_coincident(*s, g, true);
   else return 1;
   s->h20 = tl_h20;
   *out = s.release();

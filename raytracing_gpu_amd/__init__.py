@@ -95,6 +95,25 @@ class rt_render_args(ctypes.Structure):
                 ("stats", c_int32), ("flags", c_int32), ("seed", c_uint64)]
 
 
+class rt_ctx_options(ctypes.Structure):
+    """include/rt_hip.h rt_ctx_options: implementation choices that change no pixel (defaults from
+    rt_ctx_options_default, the measured product configuration)."""
+    _fields_ = [("world_tree", c_int32), ("quantized_tree", c_int32), ("merged_search", c_int32),
+                ("merge_order", c_int32), ("dedup_triangles", c_int32), ("shade_min", c_int32),
+                ("bins_min_items_per_lane", c_float), ("split_min_segments", c_float), ("split_order", c_int32),
+                ("cost_shift", c_int32), ("long_pct", c_float), ("pad", c_int32)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+
+
+RT_MERGE_ON, RT_MERGE_OFF, RT_MERGE_FALLBACK_ALL = range(3)
+RT_ORDER_DISTANCE, RT_ORDER_LIST, RT_ORDER_REVERSED = range(3)
+# Options every new Context starts from, on top of the library defaults (tests force the camera-ray
+# tile lists on through this; the product leaves it empty).
+DEFAULT_OPTIONS: dict = {}
+
+
 class rt_counters(ctypes.Structure):
     _fields_ = [("segments", c_uint64), ("node_tests", c_uint64), ("prim_tests", c_uint64),
                 ("samples", c_uint64), ("fallbacks", c_uint64)]
@@ -108,6 +127,9 @@ ABI = {
     "rt_ctx_create": (c_int, [c_int, POINTER(c_void_p)]),
     "rt_ctx_destroy": (c_int, [c_void_p]),
     "rt_last_error": (c_char_p, [c_void_p]),
+    "rt_ctx_options_default": (None, [POINTER(rt_ctx_options)]),
+    "rt_ctx_set_options": (c_int, [c_void_p, POINTER(rt_ctx_options)]),
+    "rt_ctx_get_options": (c_int, [c_void_p, POINTER(rt_ctx_options)]),
     "rt_owned_rows": (c_int32, [POINTER(rt_render_args), POINTER(c_int32)]),
     "rt_scene_upload": (c_int, [c_void_p, POINTER(rt_scene_soa)]),
     "rt_render_init": (c_int, [c_void_p, c_int32, c_int32, c_uint64]),
@@ -282,11 +304,34 @@ class Context:
         if rc != 0:
             raise RtError(f"rt_ctx_create(device={device}) failed with status {rc}")
         self.device = device
+        if DEFAULT_OPTIONS:
+            self.set_options(**DEFAULT_OPTIONS)
 
     def _check(self, rc: int, what: str) -> None:
         if rc != 0:
             msg = lib().rt_last_error(self._c)
             raise RtError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def options(self) -> dict:
+        o = rt_ctx_options()
+        self._check(lib().rt_ctx_get_options(self._c, ctypes.byref(o)), "rt_ctx_get_options")
+        return o.as_dict()
+
+    def set_options(self, reset: bool = False, **kw) -> dict:
+        """Change context options (include/rt_hip.h rt_ctx_options); reset=True starts from the
+        library defaults.  Upload-time options apply from the next upload.  Returns the options before."""
+        before = self.options()
+        o = rt_ctx_options()
+        if reset:
+            lib().rt_ctx_options_default(ctypes.byref(o))
+        else:
+            self._check(lib().rt_ctx_get_options(self._c, ctypes.byref(o)), "rt_ctx_get_options")
+        for k, v in kw.items():
+            if k not in before:
+                raise KeyError(f"unknown context option {k!r}")
+            setattr(o, k, v)
+        self._check(lib().rt_ctx_set_options(self._c, ctypes.byref(o)), "rt_ctx_set_options")
+        return before
 
     def upload(self, scene: Scene) -> None:
         self._check(lib().rt_scene_upload(self._c, ctypes.byref(scene.soa)), "rt_scene_upload")

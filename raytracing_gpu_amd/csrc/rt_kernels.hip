@@ -36,6 +36,7 @@
 
 #include "../../include/rt_hip.h"
 #include "rt_detmath.h"
+#include "rt_diag.h"
 #include "rt_host_geom.h"
 #include "rt_xorwow.h"
 
@@ -235,13 +236,10 @@ constexpr int kLockerSmall = 5;  // variants that park only the sample sum, fb a
 // counts, attenuation, RNG state): the widest global-memory variants, whose world query spills to
 // scratch at the 4-wave floor.  C5 F_FINAL at 3840x2159 4x4 (MI355X): 86.0 ms with 200 B of
 // scratch per lane; 81.6 ms with words 5..14 parked (140 B); 80.7 ms with the RNG state too (132 B).
-// F_CORNELL (no spills) ran 1 % slower with words 5..14 parked, so it keeps the small locker.
-#ifndef RT_PARK_CORNELL
-#define RT_PARK_CORNELL 0
-#endif
+// F_CORNELL (no spills) ran 1 % slower with words 5..14 parked, so it keeps the small locker (and at
+// 5 waves/SIMD too: 26 270-26 300 vs 26 850-26 930 Mrays/s).
 constexpr bool parks_segment_mask(int mask) {
-  return (mask & (F_LDS | F_STEP)) == 0 &&
-         ((mask & F_ALL) == F_FINAL || (mask & F_ALL) == F_ALL || (RT_PARK_CORNELL && (mask & F_ALL) == F_CORNELL));
+  return (mask & (F_LDS | F_STEP)) == 0 && ((mask & F_ALL) == F_FINAL || (mask & F_ALL) == F_ALL);
 }
 // LDS words per lane of traversal stack: render_kernel's global-memory variants without BVHs (C3's
 // list of rects and media) traverse nothing and keep none, so their locker starts at word 0.
@@ -287,46 +285,6 @@ __device__ __forceinline__ void stage_lds(const DScene& S) {
   __syncthreads();
 }
 
-
-// Diagnostic build only (-DRT_STAMPS): per-wave cycle shares of the render loop's phases
-// (s_memtime stamps, cdna_hip_programming.md section 7).  Phase = code run after the stamp.
-#ifdef RT_STAMPS
-constexpr int kStampPhases = 8;  // head, camera, world glue, node tests, prim tests, validation, scatter, one stamp
-__shared__ unsigned long long rt_stamp_acc[16][kStampPhases + 2];
-__device__ __forceinline__ void rt_stamp(int ph) {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  const unsigned long long act = __ballot(1);
-  if ((int)__lane_id() == __ffsll((long long)act) - 1) {
-    unsigned long long* a = rt_stamp_acc[threadIdx.x >> 6];
-    if (a[0] != 0) a[2 + a[1]] += t - a[0];
-    a[0] = t;
-    a[1] = (unsigned long long)ph;
-  }
-}
-#define RT_STAMP(ph) rt_stamp(ph)
-#else
-#define RT_STAMP(ph)
-#endif
-
-// Diagnostic build only (-DRT_STEP_DIAG): per-wave counts of traversal-loop iterations, lane
-// steps, shading phases and loop trips (render_kernel vs render_step_kernel).
-#ifdef RT_STEP_DIAG
-__device__ unsigned long long rt_diag[4];
-__shared__ unsigned long long rt_diag_acc[16][4];
-__device__ __forceinline__ void rt_diag_wave(int k) {  // one count per wave (first active lane)
-  const unsigned long long act = __ballot(1);
-  if ((int)__lane_id() == __ffsll((long long)act) - 1) {
-    rt_diag_acc[threadIdx.x >> 6][k] += 1;
-    if (k == 0) rt_diag_acc[threadIdx.x >> 6][1] += __popcll(act);
-  }
-}
-#define RT_DIAG(k) rt_diag_wave(k)
-#else
-#define RT_DIAG(k)
-#endif
 
 struct V {
   float x, y, z;
@@ -759,25 +717,18 @@ __device__ __forceinline__ bool bvh_exact(const DScene& S, int base, int rows, c
   }
 }
 
-// One step of the candidate search of bvh_closest: the node pair of `cur` (one 64-byte record),
-// its primitive children tested right away (leaves hold one primitive), then descend to the nearer
-// hit child (the farther one pushed on the lane's LDS stack) or pop.  Returns false once the
-// search has ended.  Candidates are ranges (prim_range): the lane keeps the one with the smallest
-// lo as the winner [blo, bhi] and the smallest lo of every other candidate in `second`; the
-// winner is certain when second > bhi (checked in bvh_settle).  Two exact candidates (lo = hi)
-// compare exactly, as bvh.h does (strictly smaller t, ties to the lower leaf rank), and the
-// loser is not kept in `second`: an exact loser of an exact winner has t >= the winner's t, so
-// when a range later displaces that winner, the winner's lo (added to `second`) covers it.
 // One candidate of the culled search (a primitive whose range test passed): the lane keeps the
 // candidate with the smallest lo as the winner [blo, bhi] and the smallest lo of every other
-// candidate in `second`.  Two exact candidates (lo = hi) compare exactly, as bvh.h does (strictly
-// smaller t, ties to the lower leaf rank), and the loser is not kept in `second`: an exact loser of
-// an exact winner has t >= the winner's t, so when a range later displaces that winner, the
-// winner's lo (added to `second`) covers it.
-// World tree (WORLD, F_WORLD): candidates of different world entries carry different entry parts
-// of the tie key (rk >> RT_WKEY_SHIFT).  An exact candidate of another entry is never dropped from
-// `second`: it bounds the closest-so-far that the reference's list passes to the winner's entry
-// (world_settle), and an exact tie across entries leaves second == bhi, so the query is not certain.
+// candidate in `second`; the winner is certain when second > bhi (checked in bvh_settle).  Two exact
+// candidates (lo = hi) of one BVH compare exactly, as bvh.h does (strictly smaller t, ties to the
+// lower leaf rank), and the loser is not kept in `second`: an exact loser of an exact winner has
+// t >= the winner's t, so when a range later displaces that winner, the winner's lo (added to
+// `second`) covers it.
+// World keys (WORLD: world_search, the world tree): candidates of different world entries carry
+// different entry parts of the tie key (rk >> RT_WKEY_SHIFT).  An exact candidate of another entry is
+// never dropped from `second`, whichever of the two arrives first: it bounds the closest-so-far that
+// the reference's list passes to the winner's entry (world_settle, world_search), and an exact tie
+// across entries leaves second == bhi, so the query is not certain -- whatever the visiting order.
 template <bool WORLD = false>
 __device__ __forceinline__ void take_candidate(float lo, float hi, int pi, int rk, float& blo, float& bhi,
                                                float& second, int& best_prim, int& best_rank) {
@@ -789,6 +740,8 @@ __device__ __forceinline__ void take_candidate(float lo, float hi, int pi, int r
       bhi = hi;
       best_prim = pi;
       best_rank = rk;
+    } else if (other) {
+      second = __builtin_fminf(second, lo);
     }
   } else if (lo < blo) {
     second = __builtin_fminf(second, blo);
@@ -1097,13 +1050,14 @@ __device__ __forceinline__ bool bvh_settle(const DScene& S, int base, int rows, 
 }
 
 // A ray whose sphere tests cannot produce a NaN root against the scene's inert media boundaries
-// (spheres with coordinates and radii below 1e6, checked at upload): finite, |o| < 1e7, 1e-12 <
-// |d|^2 < 1e8 -- then hb^2 and a*cc stay below ~1e23, and root = num / a is finite.  NaN and inf
-// fail the comparisons.
+// (spheres with coordinates and radii below 1e6, moving ones whose centre stays within 1e6 of c0 for
+// |time| < 1024, checked at upload by medium_inert): finite, |o| < 1e7, |time| < 1024, 1e-12 < |d|^2
+// < 1e8 -- then hb^2 and a*cc stay below ~1e23, and root = num / a is finite.  NaN and inf fail the
+// comparisons.
 __device__ __forceinline__ bool ray_sane(const Ray& r) {
   const float a = len2(r.d);
-  const float om = __builtin_fabsf(r.o.x) + __builtin_fabsf(r.o.y) + __builtin_fabsf(r.o.z) + __builtin_fabsf(r.tm);
-  return a > 1e-12f && a < 1e8f && om < 1e7f;
+  const float om = __builtin_fabsf(r.o.x) + __builtin_fabsf(r.o.y) + __builtin_fabsf(r.o.z);
+  return a > 1e-12f && a < 1e8f && om < 1e7f && __builtin_fabsf(r.tm) < 1024.0f;
 }
 
 // Outcome of the world tree's candidate search (F_WORLD; leaf = winning leaf, key its tie key):
@@ -1181,7 +1135,7 @@ __device__ __forceinline__ bool bvh_closest(const DScene& S, const rt_object& o,
     int sp = 0, cur = 0;
     bool overflow = false;
     for (;;) {
-      RT_DIAG(0);
+      RT_STEP_COUNT(0);
       if (!trav_step<F>(S, fb, r, oi, finv, a, rcpa, tmin, tmax, cur, sp, blo, bhi, second, best_prim, best_rank,
                         overflow, nnode, nprim))
         break;
@@ -1780,13 +1734,6 @@ struct RenderParams {
   // Camera-ray entry masks (render_kernel, list worlds; null: every entry is tested): bit w of
   // tile_mask[t] = a camera ray of tile t may hit top-level entry w.
   const uint32_t* tile_mask;
-#ifdef RT_TRACE
-  float* trace;
-  long long trace_item;
-#endif
-#ifdef RT_STAMPS
-  unsigned long long* stamps;
-#endif
 };
 
 constexpr int kBlock = 256;
@@ -1798,10 +1745,7 @@ constexpr int kTileCap = 32;   // entries per tile list (a fuller tile traverses
 constexpr int kRefill = 4;
 constexpr int kShadeMin = 60;  // render_step_kernel: default shading-phase threshold
 constexpr int kShadeMinMesh = 56;  // ... for triangle-mesh variants (48 before the triangle dedupe)
-#ifndef RT_SHADE_PASSES
-#define RT_SHADE_PASSES 2
-#endif
-constexpr int kShadePasses = RT_SHADE_PASSES;  // render_step_kernel: shading passes per phase
+constexpr int kShadePasses = 2;    // render_step_kernel: shading passes per phase (1: C2 17.2 -> 20.4 ms, 3: +0.7 %)
 constexpr unsigned kChunk = 64;  // items a wave claims per work-counter atomic
 static_assert(kChunk >= 64, "claim_items: one claim must cover a refill of every lane of a wave");
 
@@ -1868,28 +1812,14 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
 // 800x800 10x100: F_CORNELL at 135 VGPRs / 3 waves 33.2 ms, capped at 128 / 4 waves 28.6 ms; C5
 // 1280x720 8x8: F_ALL at 201 VGPRs / 2 waves 81.4 ms, at 168 / 3 waves 69.1 ms, at 128 / 4 waves
 // with spills 73.2 ms; F_FINAL (no checker code) at 4 waves 66.7 ms, at 3 waves 69.5 ms; C4 door:
-// F_MESH best uncapped, 166 VGPRs / 3 waves).  LDS variants run
-// 1024-thread workgroups, which already cap them at 128.  RT_WPE_GLOBAL overrides (experiments).
+// F_MESH best uncapped, 166 VGPRs / 3 waves, at 4 after the deferred hit record; F_CORNELL at 5 with its
+// list entries in SGPRs: 4 / 5 / 6 waves 24 470 / 26 890 / 25 290 Mrays/s).  LDS variants run
+// 1024-thread workgroups, which already cap them at 128.
 template <int F>
 constexpr int render_wpe() {
-#ifdef RT_WPE_GLOBAL
-  return (F & F_LDS) != 0 ? 1 : RT_WPE_GLOBAL;
-#else
   constexpr int feat = F & F_ALL;
-#ifndef RT_WPE_FINAL
-#define RT_WPE_FINAL 4
-#endif
-#ifndef RT_WPE_CORNELL
-#define RT_WPE_CORNELL 5
-#endif
-#ifndef RT_WPE_MESH
-#define RT_WPE_MESH 4
-#endif
   return (F & F_LDS) != 0 ? 1
-                          : (feat == F_FINAL ? RT_WPE_FINAL
-                                             : (feat == F_MESH ? RT_WPE_MESH
-                                                               : (feat == F_CORNELL ? RT_WPE_CORNELL : (feat == F_ALL ? 3 : 1))));
-#endif
+                          : (feat == F_FINAL || feat == F_MESH ? 4 : (feat == F_CORNELL ? 5 : (feat == F_ALL ? 3 : 1)));
 }
 template <int F>
 __global__ __launch_bounds__(render_block<F>()) __attribute__((amdgpu_waves_per_eu(render_wpe<F>())))
@@ -1904,14 +1834,8 @@ void render_kernel(const RenderParams P) {
     __syncthreads();
   }
   const unsigned lane = __lane_id();
-#ifdef RT_STEP_DIAG
-  if (lane < 4) rt_diag_acc[threadIdx.x >> 6][lane] = 0;
-#endif
-#ifdef RT_STAMPS
-  if (lane < kStampPhases + 2) rt_stamp_acc[threadIdx.x >> 6][lane] = 0;
-  __syncthreads();
-  RT_STAMP(0);
-#endif
+  RT_STEP_COUNT_BEGIN();
+  RT_STAMP_BEGIN();
   long long item = -1;  // -1: idle
   bool done = false;
   // cold state in the LDS locker (parks<F>): 0..2 sample sum, 3 fb, 4 owned row, 5 column,
@@ -2055,12 +1979,8 @@ void render_kernel(const RenderParams P) {
       Hit h;
       bool ended = false;
       V contrib;
-  #ifdef RT_TRACE
-      const Ray ray_in = ray;
-      const unsigned rng_in = loc.d;
-  #endif
       RT_STAMP(2);
-      RT_DIAG(2);
+      RT_STEP_COUNT(2);
       const uint32_t wmask = (depth == 0 && P.tile_mask) ? P.tile_mask[(j >> kTileShift) * P.tiles_x + (i >> kTileShift)]
                                                          : 0xffffffffu;
       // The merged candidate search on scenes rt_scene_upload marks merge_ok: only it in the F_MERGE
@@ -2074,18 +1994,6 @@ void render_kernel(const RenderParams P) {
       else
         hit_any = world_hit<F>(S, ray, h, loc, nnode, nprim, nfall, wmask);
       RT_STAMP(6);
-  #ifdef RT_TRACE
-      if (item == P.trace_item && P.trace) {
-        const unsigned k = atomicAdd((unsigned*)P.trace, 1u);
-        if (k < 255) {
-          float* e = P.trace + 16 * (k + 1);
-          e[0] = ray_in.o.x; e[1] = ray_in.o.y; e[2] = ray_in.o.z; e[3] = ray_in.d.x; e[4] = ray_in.d.y;
-          e[5] = ray_in.d.z; e[6] = ray_in.tm; e[7] = hit_any ? h.t : -1.0f; e[8] = __int_as_float(hit_any ? h.mat : -1);
-          e[9] = h.p.x; e[10] = h.p.y; e[11] = h.p.z; e[12] = __uint_as_float(rng_in); e[13] = __uint_as_float(loc.d);
-          e[14] = __int_as_float(s); e[15] = __int_as_float(depth);
-        }
-      }
-  #endif
       if (!hit_any) {
         contrib = att_get() * ld3(S.bg);
         ended = true;
@@ -2141,13 +2049,8 @@ void render_kernel(const RenderParams P) {
     }
   }
 
-#ifdef RT_STAMPS
-  RT_STAMP(0);
-  if (lane < kStampPhases) atomicAdd(P.stamps + lane, rt_stamp_acc[threadIdx.x >> 6][2 + lane]);
-#endif
-#ifdef RT_STEP_DIAG
-  if (lane < 4) atomicAdd(&rt_diag[lane], rt_diag_acc[threadIdx.x >> 6][lane]);
-#endif
+  RT_STAMP_END();
+  RT_STEP_COUNT_END();
   const unsigned long long ws = wave_sum(nseg), wm = wave_sum(nsamp);
   unsigned long long wn = 0, wp = 0, wf = 0;
   if constexpr ((F & F_STATS) != 0) {
@@ -2175,10 +2078,6 @@ void render_kernel(const RenderParams P) {
 // (bvh_settle, finalize), scatter, sample / item bookkeeping, refill from the work counter,
 // the next camera ray and the next query's setup.  Per lane the sequence of RNG draws and float
 // operations is exactly render_kernel's, so frame buffers are bit-identical.
-#ifdef RT_WAVE_TIMES
-__device__ unsigned long long rt_wave_times[3 * 8192];  // per wave: start, global work exhausted, end (s_memtime)
-__device__ unsigned rt_wave_count;
-#endif
 template <int F>
 __global__ __launch_bounds__(render_block<F>()) __attribute__((amdgpu_waves_per_eu(render_wpe<F>())))
 void render_step_kernel(const RenderParams P) {
@@ -2196,14 +2095,8 @@ void render_step_kernel(const RenderParams P) {
     __syncthreads();
   }
   const unsigned lane = __lane_id();
-#ifdef RT_STEP_DIAG
-  if (lane < 4) rt_diag_acc[threadIdx.x >> 6][lane] = 0;
-#endif
-#ifdef RT_STAMPS
-  if (lane < kStampPhases + 2) rt_stamp_acc[threadIdx.x >> 6][lane] = 0;
-  __syncthreads();
-  RT_STAMP(0);
-#endif
+  RT_STEP_COUNT_BEGIN();
+  RT_STAMP_BEGIN();
   const rt_object obj = ro<F>(S.objects)[ro<F>(S.world)[0]];
   const int tbase = (F & F_WORLD) != 0 ? S.wt_fb : obj.c;  // traversal tree of the world's BVH / the world tree
   const float tmin = 0.001f, tmax = __builtin_inff();  // render.h:63
@@ -2267,17 +2160,14 @@ void render_step_kernel(const RenderParams P) {
   const rt_camera& C = S.cam;
   unsigned long long chunk_base = 0;  // wave-uniform: next unclaimed item of the wave's chunk
   unsigned chunk_left = 0;
-#ifdef RT_WAVE_TIMES
-  unsigned long long wt0, wt1 = 0;
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wt0)::"memory");
-#endif
+  RT_WAVE_T0();
 
   for (;;) {
     // Shading passes: a camera ray answered by its tile's candidate list (mode 2 right after the
     // setup) is shaded in another pass of the same phase, so the traversal loop that follows
     // starts with every lane traversing.
     for (int pass = 0;; ++pass) {
-      RT_DIAG(2);
+      RT_STEP_COUNT(2);
       // ---- shading phase: finish the ended queries (render.h:60-77)
       RT_STAMP(7);  // back-to-back pair: phase 7 = the cost of one stamp per loop trip
       RT_STAMP(5);
@@ -2415,9 +2305,7 @@ void render_step_kernel(const RenderParams P) {
         if (item < 0 && !done) {
           if (mine >= P.total_items) {
             done = true;
-#ifdef RT_WAVE_TIMES
-            if (wt1 == 0) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wt1)::"memory");
-#endif
+            RT_WAVE_EXHAUSTED();
           } else {
             unsigned long long pos = mine;
             int sa = 0;
@@ -2551,20 +2439,16 @@ void render_step_kernel(const RenderParams P) {
     if (__ballot(mode != 0) == 0) break;  // no item left for any lane of the wave (mode 2: a listed camera ray)
     // ---- traversal steps until shade_min lanes wait (or none traverses)
     for (;;) {
-      RT_DIAG(3);
+      RT_STEP_COUNT(3);
       // several traversal steps per check of the shading condition, same VGPRs (same box, Mrays/s at
       // 1 / 2 / 3 / 4 steps: C2 14 538 / 14 713 / 14 829 / 14 843, C4 11 180 / 11 247 (before the
       // triangle dedupe) and 14 095 / 14 051 / 13 990 after it); the opt-in world-tree variants keep
       // one (more spills with two)
-#ifdef RT_TRAV_UNROLL
-      constexpr int kUnroll = RT_TRAV_UNROLL;
-#else
       constexpr int kUnroll = (F & F_WORLD) != 0 ? 1 : ((F & F_TRI) != 0 ? 2 : 4);
-#endif
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u)
       if (mode == 1) {
-        RT_DIAG(0);
+        RT_STEP_COUNT(0);
         if (!trav_step<F>(S, tbase, ray, oi, finv, qa, rcpa, tmin, tmax, cur, sp, best, bhi, second, best_prim,
                           best_rank, overflow, nnode, nprim))
           mode = 2;
@@ -2574,29 +2458,9 @@ void render_step_kernel(const RenderParams P) {
     }
   }
 
-#ifdef RT_STEP_DIAG
-  if (lane < 4) atomicAdd(&rt_diag[lane], rt_diag_acc[threadIdx.x >> 6][lane]);
-#endif
-#ifdef RT_STAMPS
-  RT_STAMP(0);
-  if (lane < kStampPhases) atomicAdd(P.stamps + lane, rt_stamp_acc[threadIdx.x >> 6][2 + lane]);
-#endif
-#ifdef RT_WAVE_TIMES
-  {
-    unsigned long long wt2;
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(wt2)::"memory");
-    const unsigned long long any1 = __ballot(wt1 != 0);
-    const unsigned long long e1 = any1 ? __shfl(wt1, __ffsll((long long)any1) - 1, 64) : 0ull;
-    if (lane == 0) {
-      const unsigned k = atomicAdd(&rt_wave_count, 1u);
-      if (k < 8192) {
-        rt_wave_times[3 * k] = wt0;
-        rt_wave_times[3 * k + 1] = e1;
-        rt_wave_times[3 * k + 2] = wt2;
-      }
-    }
-  }
-#endif
+  RT_STEP_COUNT_END();
+  RT_STAMP_END();
+  RT_WAVE_END();
   const unsigned long long ws = wave_sum(nseg), wm = wave_sum(nsamp);
   unsigned long long wn = 0, wp = 0, wf = 0;
   if constexpr ((F & F_STATS) != 0) {
@@ -2950,6 +2814,7 @@ __global__ __launch_bounds__(kBlock) void bin_masks_kernel(const float4* __restr
 // ====================================================================== host side (C ABI)
 struct rt_ctx {
   int device = 0;
+  rt_ctx_options opt{};  // rt_ctx_set_options (defaults: rt_ctx_options_default)
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::string err;
@@ -3043,11 +2908,6 @@ struct Variant {
 #define RT_VARIANT(m) {m, (const void*)render_kernel<m>}
 #define RT_VARIANT_STEP(m) {m, (const void*)render_step_kernel<m>}
 const Variant kVariants[] = {
-#if defined(RT_ONLY_MASK) && defined(RT_ONLY_STEP)  // ISA experiments: one stepwise instantiation
-    RT_VARIANT_STEP(RT_ONLY_MASK),
-#elif defined(RT_ONLY_MASK)  // register-pressure experiments (scripts/isa_meta.py --only): one instantiation
-    RT_VARIANT(RT_ONLY_MASK),
-#else
     RT_VARIANT_STEP(F_SPHERES | F_LDS | F_STEP),
     RT_VARIANT_STEP(F_SPHERES | F_STEP),
     RT_VARIANT_STEP(F_MESH | F_STEP),
@@ -3074,7 +2934,6 @@ const Variant kVariants[] = {
     RT_VARIANT(F_MESH | F_EXACT),
     RT_VARIANT(F_FINAL),
     RT_VARIANT(F_FINAL | F_MERGE),
-#endif
 };
 #undef RT_VARIANT
 #undef RT_VARIANT_STEP
@@ -3268,7 +3127,7 @@ struct SahBuilder {
 };
 
 int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<rt_prim>& prims,
-                         std::vector<rt_bvh_node>& nodes, std::vector<float2>& pmargin, int* n_pairs) {
+                         std::vector<rt_bvh_node>& nodes, std::vector<float2>& pmargin, int* n_pairs, bool dedup) {
   const int inner = (1 << rows) - 1, last0 = (1 << (rows - 1)) - 1;
   std::vector<int> members;
   for (int k = last0; k < inner; ++k) {
@@ -3317,9 +3176,9 @@ int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<
   // visits in its depth-first left-first order: the lowest leaf rank whose chain passes.  The
   // candidate search only needs that member; members are in rank order, so the first of each group
   // stays in the tree.  The settle validates the kept member's chain; if it fails the query re-runs
-  // on the exact visit set, where a later member may win (RT_NO_DEDUP=1 keeps every member).
+  // on the exact visit set, where a later member may win (options.dedup_triangles = 0 keeps every member).
   std::vector<int> kept;
-  if (!getenv("RT_NO_DEDUP")) {
+  if (dedup) {
     std::set<std::array<uint32_t, 9>> seen;
     for (int id : members) {
       if ((prims[id].type & 0xff) == RT_PRIM_TRIANGLE) {
@@ -3417,15 +3276,7 @@ int sort_scatter(rt_ctx* c, long long n, const unsigned* base, uint32_t* out) {
 // `segs` segments in all): perm, the long prefix and the split items.  Built when the configuration
 // is rendered again, so a single draw() does not pay the host sort.
 int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs) {
-  if (const char* e = getenv("RT_ITEM_COST_OUT")) {  // diagnostic: per-item segment counts
-    std::vector<uint16_t> ic((size_t)items);
-    HIPCHK(c, hipMemcpyAsync(ic.data(), c->item_cost, ic.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (FILE* fo = fopen(e, "wb")) {
-      fwrite(ic.data(), sizeof(uint16_t), ic.size(), fo);
-      fclose(fo);
-    }
-  }
+  RT_DIAG_ITEM_COSTS(c, items);  // diagnostic builds only (rt_diag.h): per-item segment counts to a file
   // Every item in descending cost buckets of 8 segments, the natural (spatially coherent) order
   // inside a bucket (a stable counting sort on the device; the top bucket 255 holds every item of
   // >= 2040 segments); the top ~2 % by cost are the "long" prefix whose waves run at raised
@@ -3446,7 +3297,7 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
   }
   int shift = 3;
   while (shift < 8 && (cmax >> shift) > 255u) ++shift;
-  if (const char* e = getenv("RT_COST_SHIFT")) shift = std::max(0, std::min(12, atoi(e)));  // tuning
+  if (c->opt.cost_shift >= 0) shift = std::min(12, c->opt.cost_shift);  // tuning
   cost_key_kernel<<<(unsigned)((items + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
       c->item_cost, (unsigned long long)items, shift, keys);
   HIPCHK(c, hipGetLastError());
@@ -3466,8 +3317,7 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
   if (int rc = sort_scatter(c, items, c->order_tab, c->perm)) return rc;
   // completed before returning (base is on this stack): the next launch (same stream) reads perm
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  double pct = 2.0;
-  if (const char* e = getenv("RT_LONG_PCT")) pct = atof(e);  // tuning
+  const double pct = c->opt.long_pct;
   const long long want = (long long)((double)items * pct / 100.0);
   long long nl = 0;  // whole buckets from the top while they fit in `want`
   for (int v = 255; v >= 0 && nl + hist[(size_t)v] <= want; --v) nl += hist[(size_t)v];
@@ -3488,10 +3338,15 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
     // 8.54, 48: 8.39, 231: 8.57; N = 1 (36, 925) 48: 16.56, 462: 16.53.  1 x 100: N = 8 85: 3.08,
     // 100: 2.81, 120: 2.79; N = 4 100: 5.39, 150: 5.28, 200: 5.31, 250: 6.27; N = 2 200: 10.93,
     // 300: 9.09, 400: 11.32; N = 1 200: 21.59, 300: 16.69, 400: 18.44.
+    // Round 5: the 48-segment band reaches up to 48 items per lane (was 24).  C4 (door 1920x1079,
+    // 16 x 16) as rank of N = 4 has 31.7 items per lane, and "half a lane's share" (~574 segments)
+    // split almost nothing: its warm share ran 27.9 ms against an ideal 20; at 48 segments 20.7 ms
+    // (N = 1 / 2 / 8 unchanged within 1 %).  C2's only case in the new band, N = 1 (36 per lane),
+    // measured the same at 48 and 462 in round 3.
     const double share = (double)segs / lanes, per_lane = (double)items / lanes;
-    double thr = spp <= 16 ? (per_lane < 6.0 ? 32.0 : per_lane < 24.0 ? 48.0 : std::max(32.0, 0.5 * share))
+    double thr = spp <= 16 ? (per_lane < 6.0 ? 32.0 : per_lane < 48.0 ? 48.0 : std::max(32.0, 0.5 * share))
                            : std::min(3.0 * spp, std::max(1.04 * spp, 0.85 * share));
-    if (const char* e = getenv("RT_SPLIT_MIN_SEGMENTS")) thr = atof(e);  // tuning
+    if (c->opt.split_min_segments > 0.0f) thr = c->opt.split_min_segments;  // tuning, tests
     const long long bt = (long long)std::ceil(thr / (double)(1 << shift));
     long long ns = 0;
     for (long long v = 255; v >= bt && v >= 0; --v) ns += hist[(size_t)v];  // bt > 255: no split
@@ -3528,6 +3383,7 @@ int rt_ctx_create(int hip_device, rt_ctx** out) {
   *out = nullptr;
   rt_ctx* c = new rt_ctx;
   c->device = hip_device;
+  rt_ctx_options_default(&c->opt);
   int rc = RT_OK;
   auto chk = [&](hipError_t e, const char* what) {
     if (e != hipSuccess && rc == RT_OK) rc = fail(c, RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -3610,6 +3466,45 @@ int rt_ctx_destroy(rt_ctx* c) {
 }
 
 const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void rt_ctx_options_default(rt_ctx_options* o) {
+  if (!o) return;
+  *o = rt_ctx_options{};
+  o->world_tree = 0;
+  o->quantized_tree = 1;
+  o->merged_search = RT_MERGE_ON;
+  o->merge_order = RT_ORDER_DISTANCE;
+  o->dedup_triangles = 1;
+  o->shade_min = 0;
+  o->bins_min_items_per_lane = 6.0f;
+  o->split_min_segments = 0.0f;
+  o->split_order = 1;
+  o->cost_shift = -1;
+  o->long_pct = 2.0f;
+}
+
+int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
+  if (!c || !o) return RT_ERR_ARG;
+  if (o->merged_search < RT_MERGE_ON || o->merged_search > RT_MERGE_FALLBACK_ALL ||
+      o->merge_order < RT_ORDER_DISTANCE || o->merge_order > RT_ORDER_REVERSED || o->shade_min < 0 ||
+      o->shade_min > 64 || !(o->bins_min_items_per_lane >= 0.0f) || !(o->split_min_segments >= 0.0f) ||
+      o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f))
+    return fail(c, RT_ERR_ARG, "bad context options");
+  c->opt = *o;
+  // the schedule and split thresholds come from the options: every configuration starts cold again
+  std::fill(c->perm_key, c->perm_key + rt_ctx::kKey, -1LL);
+  std::fill(c->pending_key, c->pending_key + rt_ctx::kKey, -1LL);
+  c->split_state = -1;
+  c->n_split = 0;
+  c->order_ok = false;
+  return RT_OK;
+}
+
+int rt_ctx_get_options(const rt_ctx* c, rt_ctx_options* o) {
+  if (!c || !o) return RT_ERR_ARG;
+  *o = c->opt;
+  return RT_OK;
+}
 
 int32_t rt_owned_rows(const rt_render_args* a, int32_t* rows) {
   if (!a || a->band_rows <= 0 || a->band_stride <= 0) return 0;
@@ -3717,8 +3612,10 @@ bool object_box(const rt_scene_soa* s, int oi, float t0, float t1, rth::Box& out
 // second boundary query returns nothing or t1 itself) unless its boundary root is NaN, which a
 // sane ray (ray_sane) cannot produce.  Leaves: 4 float4 each (see DScene::wleaf).
 // A constant medium that never reaches its RNG draw for a sane ray (ray_sane): its boundary is a
-// sphere (or a moving sphere with time1 != time0) with coordinates and radius below 1e6, whose second
-// boundary query repeats the first root (H1, sphere.h:51) -- see sphere_boundary_no_hit.
+// sphere with coordinates and radius below 1e6, whose second boundary query repeats the first root
+// (H1, sphere.h:51) -- see sphere_boundary_no_hit -- or a moving sphere whose centre c0 + (tm - t0) /
+// dt * d stays within 1e6 of c0 for every sane ray time (|tm| < 1024): a tiny shutter span dt would
+// let the centre run off to where the boundary root overflows to NaN, and NaN reaches the draw.
 static bool medium_inert(const rt_scene_soa* s, const rt_object& o) {
   if (o.kind != RT_OBJ_MEDIUM || o.a < 0 || o.a >= s->n_objects) return false;
   const rt_object& bo = s->objects[o.a];
@@ -3729,7 +3626,9 @@ static bool medium_inert(const rt_scene_soa* s, const rt_object& o) {
   const int np = ty == RT_PRIM_SPHERE ? 4 : 9;
   for (int k = 0; k < np; ++k)
     if (!(std::fabs(q.p[k]) < 1e6f)) return false;
-  return ty == RT_PRIM_SPHERE || q.p[8] != 0.0f;
+  if (ty == RT_PRIM_SPHERE) return true;
+  const double dmax = std::max(std::fabs((double)q.p[4]), std::max(std::fabs((double)q.p[5]), std::fabs((double)q.p[6])));
+  return q.p[8] != 0.0f && (1024.0 + std::fabs((double)q.p[7])) / std::fabs((double)q.p[8]) * dmax < 1e6;
 }
 
 static bool build_world_tree(const rt_scene_soa* s, const std::vector<rt_prim>& prims, std::vector<rt_bvh_node>& nodes,
@@ -3938,7 +3837,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
     o.c = -1;
     if (o.kind == RT_OBJ_MEDIUM && medium_inert(s, o)) o.c = 1;  // object_query skips it for sane rays
     if (o.kind == RT_OBJ_BVH) {
-      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes, pmargin, &tree_pairs[k]);
+      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes, pmargin, &tree_pairs[k], c->opt.dedup_triangles != 0);
       if (fast < 0) return fail(c, RT_ERR_SCENE, "malformed reference bvh");
       o.c = fast;
     }
@@ -3962,13 +3861,13 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   for (int w = 1; w < s->n_world; ++w) world_step = world_step && s->objects[s->world[w]].kind == RT_OBJ_PRIM;
   std::vector<float4> wleaf, wxf;
   int wt_fb = -1, w_media = 0, w_inert = 0;
-  // The world tree is opt-in (RT_WORLD_TREE=1): measured slower than render_kernel's entry loop on
+  // The world tree is opt-in (options.world_tree): measured slower than render_kernel's entry loop on
   // both list-world configs (MI355X: C5 3840x2159 4x4 97.2 ms vs 78.4; C3 800x800 10x10 24.7 vs 19.1)
-  const bool world_tree = !world_step && getenv("RT_WORLD_TREE") && atoi(getenv("RT_WORLD_TREE")) != 0 &&
+  const bool world_tree = !world_step && c->opt.world_tree != 0 &&
                           build_world_tree(s, prims, nodes, wleaf, wxf, wt_fb, w_media, w_inert);
   std::vector<uint32_t> qnodes;
   int q_pairs = 0, q_ebias = 0;
-  if (world_step && !getenv("RT_NO_QLDS")) {  // the world BVH's traversal tree, quantized (F_QLDS)
+  if (world_step && c->opt.quantized_tree != 0) {  // the world BVH's traversal tree, quantized (F_QLDS)
     // (the tree's own record count: coincident triangles are not leaves of it)
     const rt_object& wo = objects[(size_t)s->world[0]];
     const int np = tree_pairs[(size_t)s->world[0]];
@@ -4001,9 +3900,10 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   d.w_media = w_media;
   d.w_inert = w_inert;
   // world_search applies: a list of primitives, BVHs (up to 2^20 leaves) and instances of them, and
-  // inert media (RT_NO_MERGE: the entry loop; A/B experiments)
-  // (RT_MERGE_FALLBACK: the search runs, then every query takes the exact list; tests)
-  d.merge_ok = !world_step && s->n_world >= 2 && s->n_world < (1 << (31 - RT_WKEY_SHIFT)) && !getenv("RT_NO_MERGE");
+  // inert media (options.merged_search: RT_MERGE_OFF keeps the entry loop; RT_MERGE_FALLBACK_ALL runs
+  // the search, then every query takes the exact list -- tests)
+  d.merge_ok = !world_step && s->n_world >= 2 && s->n_world < (1 << (31 - RT_WKEY_SHIFT)) &&
+               c->opt.merged_search != RT_MERGE_OFF;
   for (int w = 0; w < s->n_world && d.merge_ok; ++w) {
     const rt_object& o = s->objects[s->world[w]];
     const rt_object& x = o.kind == RT_OBJ_XFORM ? s->objects[o.a] : o;
@@ -4011,17 +3911,18 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
     else if (x.kind == RT_OBJ_BVH) d.merge_ok = x.b <= RT_WKEY_SHIFT;
     else d.merge_ok = x.kind == RT_OBJ_PRIM;
   }
-  if (d.merge_ok && getenv("RT_MERGE_FALLBACK")) d.merge_ok = 2;
+  if (d.merge_ok && c->opt.merged_search == RT_MERGE_FALLBACK_ALL) d.merge_ok = 2;
   // world_search's visiting order (the winner does not depend on it: tie keys carry the list
   // position): the primitive entries first (one test each; their hits cull the traversals after
   // them), then the BVH and instance entries nearest first by the distance from the camera's origin
   // to their world-space box over the shutter, then the (inert) media.  C5, same box, Mrays/s: list
   // order 5 010-5 017, primitives first 5 036-5 044, primitives first + ground, door, instance (the
-  // distance order) 5 093, + door, instance, ground 5 086, BVHs first 4 960.  RT_MERGE_ORDER=list
-  // keeps list order; an explicit permutation "3,0,1,..." is taken as given.
+  // distance order) 5 093, + door, instance, ground 5 086, BVHs first 4 960.  options.merge_order:
+  // RT_ORDER_LIST keeps list order, RT_ORDER_REVERSED reverses it (tests: both arrival orders of a tie).
   std::vector<int32_t> worder((size_t)s->n_world);
   for (int w = 0; w < s->n_world; ++w) worder[(size_t)w] = w;
-  {
+  if (c->opt.merge_order == RT_ORDER_REVERSED) std::reverse(worder.begin(), worder.end());
+  if (c->opt.merge_order == RT_ORDER_DISTANCE) {
     const float t0 = std::min(s->camera.time0, s->camera.time1), t1 = std::max(s->camera.time0, s->camera.time1);
     auto rank = [&](int w) -> double {  // < 0: primitive; distance: BVH / instance; +inf: medium / no box
       const rt_object& o = s->objects[s->world[w]];
@@ -4038,23 +3939,6 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
     std::vector<double> key((size_t)s->n_world);
     for (int w = 0; w < s->n_world; ++w) key[(size_t)w] = rank(w);
     std::stable_sort(worder.begin(), worder.end(), [&](int x, int y) { return key[(size_t)x] < key[(size_t)y]; });
-  }
-  if (const char* e = getenv("RT_MERGE_ORDER")) {
-    if (!strcmp(e, "list")) {
-      for (int w = 0; w < s->n_world; ++w) worder[(size_t)w] = w;
-    } else {
-      std::vector<int32_t> p;
-      for (const char* q = e; *q;) {
-        p.push_back((int32_t)strtol(q, (char**)&q, 10));
-        if (*q == ',') ++q;
-        else break;
-      }
-      std::vector<int32_t> chk(p);
-      std::sort(chk.begin(), chk.end());
-      bool perm = (int)p.size() == s->n_world;
-      for (int w = 0; perm && w < s->n_world; ++w) perm = chk[(size_t)w] == w;
-      if (perm) worder = p;
-    }
   }
   if ((rc = upload(c, worder.data(), worder.size(), &d.worder))) return rc;
   if (q_pairs > 0 && (rc = upload(c, qnodes.data(), qnodes.size(), &d.qnodes))) return rc;
@@ -4228,8 +4112,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     HIPCHK(c, hipMalloc((void**)&c->perm, (size_t)items * sizeof(uint32_t)));
     c->item_cap = items;
   }
-  long long order_cap = 8LL * c->cus * 1024;
-  if (const char* e = getenv("RT_COST_ORDER_ITEMS")) order_cap = atoll(e);  // tuning
+  const long long order_cap = 8LL * c->cus * 1024;
   if (!sched && have_cost && items < order_cap)
     std::stable_sort(rm.begin() + rows, rm.end(), [&](int x, int y) { return c->host_cost[rm[x]] > c->host_cost[rm[y]]; });
   // Per-launch host work kept off the repeat path: the row tables are uploaded only when they
@@ -4354,8 +4237,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     // recording launch's counts (the long samples of a small share start with the launch instead of
     // trailing it).  Built once per recording; results do not depend on the order.
     const long long rest = items - (long long)c->n_split;
-    const char* oe = getenv("RT_SPLIT_ORDER");  // tuning: 0 = samples in item order, then the rest
-    if (split_mode == 2 && c->rest_n == rest && !(oe && atoi(oe) == 0)) {
+    if (split_mode == 2 && c->rest_n == rest && c->opt.split_order != 0) {  // 0: samples in item order, then the rest
       const long long total = need + rest;
       if (!c->order_ok) {
         if (total > c->order_cap) {
@@ -4399,7 +4281,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     if (split_mode == 2) P.total_items = (unsigned long long)need + (unsigned long long)(items - (long long)c->n_split);
   }
   P.item_cost = (sched && !have_perm) ? c->item_cost : nullptr;
-  if (const char* e = getenv("RT_SHADE_MIN")) P.shade_min = std::max(1, std::min(64, atoi(e)));
+  if (c->opt.shade_min > 0) P.shade_min = c->opt.shade_min;
   if (check) {
     if (!c->dbg) {
       HIPCHK(c, hipMalloc((void**)&c->dbg, 16 * sizeof(float) * kAuditCap + 64));
@@ -4453,9 +4335,16 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   // multi-GPU image) the launch ends with its longest items and the lists made that tail longer
   // (C2, one GPU rendering each rank's share: N = 4 (9.2 items per resident lane) 5.24 ms with
   // lists vs 5.94 without, N = 8 (4.6 per lane) 4.03 vs 3.51 ms).
-  double bins_min = 6.0;  // items per resident lane
-  if (const char* e = getenv("RT_BINS_MIN_ITEMS_PER_LANE")) bins_min = atof(e);  // tuning
-  const double lanes = (double)c->cus * std::max(1, c->blocks_per_cu[var]) * bs;
+  const double bins_min = c->opt.bins_min_items_per_lane;  // items per resident lane (default 6)
+  // resident workgroups per CU: from the context's occupancy table, except for the variants whose
+  // LDS holds the scene's tables after the locker (their size is the scene's)
+  int bpc = std::max(1, c->blocks_per_cu[var]);
+  if (tables_var) {
+    int b = 0;
+    HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kVariants[var].fn, bs, shmem));
+    bpc = std::max(1, b);
+  }
+  const double lanes = (double)c->cus * bpc * bs;
   if (cull && (vm & F_STEP) != 0 && c->bin_n > 0 && (double)P.total_items >= bins_min * lanes) {
     const long long tkey[3] = {c->scene_gen, a->width, a->height};
     if (!std::equal(tkey, tkey + 3, c->tiles_key)) {
@@ -4476,42 +4365,15 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     P.tiles_x = tx;
     P.tile_cap = kTileCap;
   }
-  const long long resident = (long long)c->cus * std::max(1, c->blocks_per_cu[var]);
+  const long long resident = (long long)c->cus * bpc;
   // Persistent grid: every resident workgroup, even when there are fewer items than lanes (a
   // rank of a multi-GPU run): waves take items dynamically, so the items spread over all CUs
   // instead of packing into the first ceil(items / block) of them.
-#ifdef RT_GRID_PACKED
-  const long long cap = (long long)((P.total_items + bs - 1) / bs);
-#else
-  const long long cap = resident;
-#endif
-  const unsigned blocks = (unsigned)std::max(1LL, std::min(resident, cap));
+  const unsigned blocks = (unsigned)std::max(1LL, resident);
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-#ifdef RT_STAMPS
-  static unsigned long long* sbuf = nullptr;
-  if (!sbuf) (void)hipMalloc((void**)&sbuf, 8 * sizeof(unsigned long long));
-  (void)hipMemsetAsync(sbuf, 0, 8 * sizeof(unsigned long long), c->stream);
-  P.stamps = sbuf;
-#endif
-#ifdef RT_TRACE
-  static float* tbuf = nullptr;
-  if (!tbuf) hipMalloc((void**)&tbuf, 16 * 256 * sizeof(float));
-  hipMemsetAsync(tbuf, 0, 16 * 256 * sizeof(float), c->stream);
-  P.trace = getenv("RT_TRACE_ITEM") ? tbuf : nullptr;
-  P.trace_item = getenv("RT_TRACE_ITEM") ? atoll(getenv("RT_TRACE_ITEM")) : -1;
-#endif
-#ifdef RT_STEP_DIAG
-  {
-    const unsigned long long z[4] = {0, 0, 0, 0};
-    hipMemcpyToSymbol(HIP_SYMBOL(rt_diag), z, sizeof(z));
-  }
-#endif
-#ifdef RT_WAVE_TIMES
-  {
-    const unsigned z = 0;
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(rt_wave_count), &z, sizeof(z));
-  }
-#endif
+  RT_STEP_COUNT_HOST_RESET();
+  RT_STAMP_HOST_RESET();
+  RT_WAVE_HOST_RESET();
   void* kargs[] = {&P};
   HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), kargs, shmem, c->stream));
   HIPCHK(c, hipGetLastError());
@@ -4552,43 +4414,9 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     counters->samples = host_cnt[4];
     counters->fallbacks = host_cnt[5];
   }
-#ifdef RT_WAVE_TIMES
-  if (const char* out = getenv("RT_WAVE_TIMES_OUT")) {
-    std::vector<unsigned long long> wt(3 * 8192);
-    unsigned n = 0;
-    (void)hipMemcpyFromSymbol(&n, HIP_SYMBOL(rt_wave_count), sizeof(n));
-    (void)hipMemcpyFromSymbol(wt.data(), HIP_SYMBOL(rt_wave_times), wt.size() * sizeof(unsigned long long));
-    FILE* fo = fopen(out, "wb");
-    fwrite(wt.data(), sizeof(unsigned long long), 3 * (size_t)std::min(n, 8192u), fo);
-    fclose(fo);
-  }
-#endif
-#ifdef RT_STEP_DIAG
-  {
-    unsigned long long h[4];
-    hipMemcpyFromSymbol(h, HIP_SYMBOL(rt_diag), sizeof(h));
-    fprintf(stderr, "RT_STEP_DIAG var=%d trav_wave_iters=%llu trav_lane_steps=%llu shade_phases=%llu trips=%llu\n", var,
-            h[0], h[1], h[2], h[3]);
-  }
-#endif
-#ifdef RT_STAMPS
-  if (getenv("RT_STAMPS_OUT")) {
-    unsigned long long hs[8];
-    (void)hipMemcpy(hs, sbuf, sizeof(hs), hipMemcpyDeviceToHost);
-    FILE* fo = fopen(getenv("RT_STAMPS_OUT"), "ab");
-    fwrite(hs, sizeof(hs), 1, fo);
-    fclose(fo);
-  }
-#endif
-#ifdef RT_TRACE
-  if (P.trace) {
-    std::vector<float> hb(16 * 256);
-    hipMemcpy(hb.data(), tbuf, hb.size() * sizeof(float), hipMemcpyDeviceToHost);
-    FILE* fo = fopen(getenv("RT_TRACE_OUT"), "wb");
-    fwrite(hb.data(), sizeof(float), hb.size(), fo);
-    fclose(fo);
-  }
-#endif
+  RT_WAVE_HOST_WRITE();
+  RT_STEP_COUNT_HOST_PRINT(var);
+  RT_STAMP_HOST_WRITE();
   if (host_cnt[4] != (unsigned long long)a->spp * (unsigned long long)items)  // split samples: items != work items
     return fail(c, RT_ERR_HIP, "render kernel did not complete every sample");
   return RT_OK;

@@ -562,6 +562,52 @@ bool scene_final(rt_scene_host& s, const rt_scene_assets* a) {
   return true;
 }
 
+// Test scenes "coincident" / "coincident_step" (not in scenes.h): parity fixtures of the list and
+// BVH tie rules, restated in the oracle (build_coincident).  "coincident": xy_rects in the plane z = 0
+// in three kinds of list entries -- a primitive, members of a reference BVH and a translate(rotate_y(..,
+// 0)) instance (rotate_y by 0 and a translation in x, y leave the ray's z terms exact) -- so world
+// queries meet exact ties across entries (hittable_list.h:23-39: the later entry wins) and inside the
+// BVH (the first visited wins).  "coincident_step": render_step_kernel's world shape (a BVH, then
+// primitives): a triangle repeated bit for bit inside the BVH and once more after it (Moller-Trumbore's
+// t depends on v0, e0, e1 only, so equal triangles tie exactly: the H16 duplicates' case).
+void scene_coincident(rt_scene_host& s, bool step) {
+  set_bg(s, kSky, 16.0f / 9.0f);
+  SceneRng g;
+  const int red = s.lam(mk(0.8f, 0.1f, 0.1f)), green = s.lam(mk(0.1f, 0.8f, 0.1f));
+  const int yellow = s.lam(mk(0.8f, 0.8f, 0.1f)), blue = s.lam(mk(0.1f, 0.2f, 0.8f));
+  const int cyan = s.lam(mk(0.1f, 0.8f, 0.8f)), grey = s.lam(mk(0.5f, 0.5f, 0.5f));
+  const int metal = s.mat(RT_MAT_METAL, s.solid(mk(0.8f, 0.8f, 0.8f)), 0.05f);
+  const int glass = s.mat(RT_MAT_DIELECTRIC, -1, 1.5f);
+  const int first = (int)s.prims.size();
+  if (step) {
+    const float uv[6] = {0, 0, 1, 0, 0, 1};
+    const F3 a = mk(-1.0f, -1.5f, 0.0f), b = mk(2.0f, -1.5f, 0.0f), c = mk(-1.0f, 0.5f, 0.0f), d = mk(2.0f, 0.5f, 0.0f);
+    s.tri(a, b, c, uv, nullptr, green);
+    s.tri(b, d, c, uv, nullptr, blue);
+    s.sphere(mk(2.2f, -0.3f, -0.8f), 0.5f, metal);
+    s.tri(a, b, c, uv, nullptr, yellow);  // the first triangle again
+    s.sphere(mk(-2.0f, 0.2f, -1.0f), 0.6f, glass);
+    const int bvh = s.bvh(first, 5, 0.0f, 1.0f, g);
+    const int again = s.object(RT_OBJ_PRIM, s.tri(a, b, c, uv, nullptr, red), 0);  // and after the BVH
+    const int ground = s.object(RT_OBJ_PRIM, s.sphere(mk(0.0f, -101.7f, 0.0f), 100.0f, grey), 0);
+    s.world = {bvh, again, ground};
+  } else {
+    s.rect(RT_PRIM_RECT_XY, -1.0f, 2.0f, -1.5f, 0.5f, 0.0f, green);
+    s.rect(RT_PRIM_RECT_XY, -3.0f, 3.0f, 0.8f, 2.0f, 0.5f, blue);
+    s.sphere(mk(2.2f, -0.3f, -0.8f), 0.5f, metal);
+    s.rect(RT_PRIM_RECT_XY, -0.5f, 0.7f, -1.2f, -0.2f, 0.0f, yellow);
+    s.rect(RT_PRIM_RECT_XZ, -3.0f, 3.0f, -3.0f, 3.0f, -1.6f, grey);
+    s.sphere(mk(-2.0f, 0.2f, -1.0f), 0.6f, glass);
+    const int bvh = s.bvh(first, 6, 0.0f, 1.0f, g);
+    const int prim = s.object(RT_OBJ_PRIM, s.rect(RT_PRIM_RECT_XY, -2.0f, 0.5f, -1.0f, 1.0f, 0.0f, red), 0);
+    const int ground = s.object(RT_OBJ_PRIM, s.sphere(mk(0.0f, -101.7f, 0.0f), 100.0f, grey), 0);
+    const int inst = s.xform(s.object(RT_OBJ_PRIM, s.rect(RT_PRIM_RECT_XY, -0.75f, 1.25f, -0.6f, 1.1f, 0.0f, cyan), 0),
+                             0.0f, mk(0.25f, 0.1f, 0.0f));
+    s.world = {prim, bvh, inst, ground};
+  }
+  s.camera(mk(0.3f, 0.4f, -6.0f), mk(0, 0, 0), mk(0, 1, 0), 40, 16.0f / 9.0f, 0.1f, 6.0f, 0, 1);
+}
+
 int build_named(rt_scene_host& s, const std::string& n, const rt_scene_assets* a) {
   if (n == "basic") scene_basic(s);
   else if (n == "first") scene_first(s);
@@ -577,6 +623,8 @@ int build_named(rt_scene_host& s, const std::string& n, const rt_scene_assets* a
   else if (n == "door") { if (!scene_mesh(s, a, mk(-3, 4, -5), mk(0, 1, 0))) return RT_ERR_ARG; }
   else if (n == "cup") { if (!scene_mesh(s, a, mk(0, 0, -1), mk(0, 0, 0))) return RT_ERR_ARG; }
   else if (n == "final") { if (!scene_final(s, a)) return RT_ERR_ARG; }
+  else if (n == "coincident") scene_coincident(s, false);
+  else if (n == "coincident_step") scene_coincident(s, true);
   else return RT_ERR_ARG;
   return RT_OK;
 }

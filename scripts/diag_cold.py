@@ -2,6 +2,9 @@
 rank-0 share of N = 8; then the per-item segment-count distribution (the longest item bounds a
 cold launch: a lane runs an item's samples serially).
 
+The item-cost dump needs a diagnostic build (scripts/build_ab.sh cold raytracing_gpu_amd/csrc/rt_kernels.hip
+-DRT_DIAG=8; RT_HIP_LIB=build/ab/libcold.so); the launch times do not.
+
 usage: diag_cold.py [scene W H spp nfb]
 """
 import os

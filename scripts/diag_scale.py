@@ -7,7 +7,7 @@ item schedule yet: the reference's single draw()), "warm" the best of launches 3
 is modelled from its bytes (N x the largest share's 8-bit rows) at XGMI_GBS (default 64 GB/s,
 a conservative all-gather rate for a few MB over xGMI) plus 30 us of collective latency.
 
-usage: diag_scale.py [scene W H spp nfb]
+usage: diag_scale.py [scene W H spp nfb] [--opt KEY=VALUE ...]   (context options, include/rt_hip.h)
 """
 import os
 import sys
@@ -17,9 +17,18 @@ import torch
 
 import raytracing_gpu_amd as rt
 
-scene, W, H, spp, nfb = (sys.argv[1], *[int(x) for x in sys.argv[2:6]]) if len(sys.argv) > 1 else ("big1", 1200, 800, 10, 10)
+from bench import parse_opts, scene_assets  # noqa: E402  (door mesh fixture, synthetic textures for C4 / C5)
+
+argv = [x for x in sys.argv[1:]]
+opt_items = []
+while "--opt" in argv:
+    k = argv.index("--opt")
+    opt_items.append(argv[k + 1])
+    del argv[k:k + 2]
+scene, W, H, spp, nfb = (argv[0], *[int(x) for x in argv[1:5]]) if argv else ("big1", 1200, 800, 10, 10)
 ctx = rt.Context(0)
-from bench import scene_assets  # noqa: E402  (door mesh fixture, synthetic textures for C4 / C5)
+if opt_items:
+    ctx.set_options(**parse_opts(opt_items))
 
 ctx.upload(rt.Scene.builtin(scene, **scene_assets(scene)[0]))
 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]

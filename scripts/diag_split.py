@@ -1,5 +1,5 @@
 """Diagnostic: warm (split-sample replay) launch time of C2 against the split threshold
-(RT_SPLIT_MIN_SEGMENTS), for the full frame and the rank-0 share of N = 8.
+(context option split_min_segments), for the full frame and the rank-0 share of N = 8.
 
 usage: diag_split.py [spp nfb thresholds...]
 """
@@ -22,13 +22,11 @@ for n in [int(x) for x in os.environ.get("DIAG_N", "1,8").split(",")]:
     fb = torch.empty(nfb * len(rt.owned_rows(args)) * W * 3, dtype=torch.float32, device="cuda")
     res = []
     for t in thr:
-        if t != "default":
-            os.environ["RT_SPLIT_MIN_SEGMENTS"] = t
+        ctx.set_options(split_min_segments=0.0 if t == "default" else float(t))
         ctx.upload(sc)  # new scene generation: the schedule (and its split set) is rebuilt
         ms = []
         for _ in range(5):
             ctx.render(args, fb.data_ptr())
             ms.append(ctx.last_render_ms())
-        os.environ.pop("RT_SPLIT_MIN_SEGMENTS", None)
         res.append(f"{t}: {min(ms[2:]):.2f}")
     print(f"N={n} {nfb}x{spp} warm ms by split threshold: " + ", ".join(res), flush=True)

@@ -1,6 +1,15 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, bench, rocprof kernel trace.  Stops at the first
-# crash-like exit (timeout, abort, segfault); a plain test failure does not stop the bench.
+# One GPU-box session, the steps named in $STEPS (default: tests smoke bench), each under its own time
+# limit; stops at the first crash-like exit (timeout, abort, segfault) and at a failed test run.
+#   STEPS="tests c2 c4 scale_c4" bash scripts/gpu_round.sh
+# Steps:
+#   tests            pytest -m gpu (TESTS="-k expr" narrows it)
+#   smoke            __graft_entry__.smoke()
+#   c2 c2x100 c3 c3full c4 c5 c5full   bench.py lines of the BASELINE configs (C2 = the default)
+#   scale_c2 scale_c4 scale_c5         scripts/diag_scale.py: every rank's share on this GPU
+#   prof             scripts/prof_all.sh: rocprofv3 kernel traces + PMC passes of C2-C5
+#   isa              scripts/isa_meta.py (registers / spills of every instantiation)
+# BENCH_ARGS is appended to every bench line (e.g. BENCH_ARGS="--opt shade_min=52").
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -11,16 +20,34 @@ run() {  # name timeout cmd...
   timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "   rc=$rc" | tee -a gpurun_out/summary.txt
-  tail -5 "gpurun_out/$name.log"
+  tail -3 "gpurun_out/$name.log"
   if crash $rc; then echo "CRASH in $name, stopping"; exit $rc; fi
-  return 0
+  return $rc
 }
-STEPS=${STEPS:-tests smoke bench prof}
-for s in $STEPS; do
+bench() {  # name args...
+  local name=$1; shift
+  run bench_$name 600 python -u bench.py "$@" ${BENCH_ARGS:-} || exit $?
+  grep -o '"value": [0-9.]*\|"kernel_ms": [0-9.]*\|"cold_ms_per_step": [0-9.]*\|"cold_value": [0-9.]*' \
+    gpurun_out/bench_$name.log | tr '\n' ' '; echo
+}
+C4="--scene door --width 1920 --height 1079 --spp 16 --nfb 16"
+C5="--scene final --width 3840 --height 2159 --spp 4 --nfb 4"
+for s in ${STEPS:-tests smoke c2}; do
   case $s in
-    tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
-    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) run bench 600 python bench.py --steps 3 --warmup 1 ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TESTS:-} || exit $? ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    c2) bench c2 ;;
+    c2x100) bench c2x100 --nfb 1 --spp 100 --no-cpu-baseline ;;
+    c3) bench c3 --scene cornell_smoke --width 800 --height 800 --no-cpu-baseline ;;
+    c3full) bench c3full --scene cornell_smoke --width 800 --height 800 --nfb 10 --spp 100 --steps 3 --warmup 2 --no-cpu-baseline ;;
+    c4) bench c4 $C4 --no-cpu-baseline ;;
+    c5) bench c5 $C5 --no-cpu-baseline ;;
+    c5full) bench c5full --scene final --width 3840 --height 2159 --spp 100 --nfb 100 --steps 1 --warmup 0 --cold-steps 1 --no-cpu-baseline --no-stats ;;
+    scale_c2) run scale_c2 600 python -u scripts/diag_scale.py || exit $? ;;
+    scale_c4) run scale_c4 600 python -u scripts/diag_scale.py door 1920 1079 16 16 || exit $? ;;
+    scale_c5) run scale_c5 600 python -u scripts/diag_scale.py final 3840 2159 4 4 || exit $? ;;
+    prof) STEP_TIMEOUT=300 bash scripts/prof_all.sh || exit $? ;;
+    isa) run isa 300 python scripts/isa_meta.py gpurun_out/isa_meta.txt || exit $? ;;
+    *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -1,8 +1,8 @@
 """Register / spill / scratch metadata of every render-kernel instantiation, from the AMDGPU
 code-object metadata of a device-only assembly build of csrc/rt_kernels.hip.
 
-usage: python scripts/isa_meta.py [OUT.txt] [--only MASK] [-DNAME ...]
-  (compiles with the product flags, ~45 s; --only MASK instantiates one render_kernel<MASK>)
+usage: python scripts/isa_meta.py [OUT.txt] [-DNAME ...]
+  (compiles with the product flags, ~60 s)
 """
 import os
 import re
@@ -24,10 +24,6 @@ def main():
     argv = sys.argv[1:]
     extra = [a for a in argv if a.startswith("-D")]
     argv = [a for a in argv if not a.startswith("-D")]
-    if "--only" in argv:
-        k = argv.index("--only")
-        extra.append(f"-DRT_ONLY_MASK={argv[k + 1]}")
-        del argv[k:k + 2]
     sys.argv = [sys.argv[0]] + argv
     with tempfile.TemporaryDirectory() as td:
         s = os.path.join(td, "rt.s")

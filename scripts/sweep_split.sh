@@ -1,5 +1,5 @@
 #!/bin/bash
-# Split-threshold sweep per share (diag_split.py), C2 1 x 100 and 10 x 10; extra env from $SWEEP_ENV.
+# Split-threshold sweep per share (diag_split.py), C2 1 x 100 and 10 x 10; extra env from $SWEEP_ENV (e.g. RT_HIP_LIB=build/ab/libX.so).
 mkdir -p gpurun_out
 o=gpurun_out/sweep.log; : > $o
 one() { echo "N=$1 ${SWEEP_ENV:-}" >> $o; env ${SWEEP_ENV:-} DIAG_N=$1 timeout -k 10 300 python scripts/diag_split.py "${@:2}" 2>/dev/null | grep warm >> $o || exit 1; }

@@ -12,9 +12,11 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     # The product uses camera-ray tile lists only for shares with >= 6 items per resident lane
-    # (rt_render); the parity tests' small images would never reach them, so the tests force them
-    # on (test_camera_lists_on_and_off covers the default threshold).
-    os.environ.setdefault("RT_BINS_MIN_ITEMS_PER_LANE", "0")
+    # (rt_render); the parity tests' small images would never reach them, so every Context the tests
+    # create forces them on (test_camera_lists_on_and_off covers the default threshold).
+    import raytracing_gpu_amd as rt
+
+    rt.DEFAULT_OPTIONS["bins_min_items_per_lane"] = 0.0
 
 
 @pytest.fixture(scope="session")
@@ -44,3 +46,12 @@ def gpu_ctx(rtlib):
     ctx = rtlib.Context(0)
     yield ctx
     ctx.close()
+
+
+@pytest.fixture
+def ctx_opts(gpu_ctx):
+    """Set rt_ctx_options on the session context for one test (include/rt_hip.h); the options are
+    restored afterwards.  Upload-time options take effect at the test's next upload."""
+    before = gpu_ctx.options()
+    yield lambda **kw: gpu_ctx.set_options(**kw)
+    gpu_ctx.set_options(**before)

@@ -293,10 +293,11 @@ def test_culled_equals_exact_asset_scenes(rtlib, gpu_ctx, scene, W, H, spp, nfb)
 
 
 @pytest.mark.parametrize("scene", ["door", "final"])
-def test_coincident_triangles_leave_the_traversal_tree(rtlib, gpu_ctx, monkeypatch, scene):
+def test_coincident_triangles_leave_the_traversal_tree(rtlib, gpu_ctx, ctx_opts, scene):
     """The door's H16 duplicates (triangles repeating an earlier one's v0, e0, e1 bit for bit) keep
     one leaf per group in the traversal trees: every float and the segment count equal the build with
-    every member (RT_NO_DEDUP=1, read at upload) and the exact visit set, with fewer primitive tests."""
+    every member (options.dedup_triangles = 0, read at upload) and the exact visit set, with fewer
+    primitive tests."""
     import os
 
     import torch
@@ -307,10 +308,7 @@ def test_coincident_triangles_leave_the_traversal_tree(rtlib, gpu_ctx, monkeypat
     W, H, spp, nfb = 320, 180, 4, 2
     out = {}
     for mode in ("dedup", "all", "exact"):
-        if mode == "all":
-            monkeypatch.setenv("RT_NO_DEDUP", "1")
-        else:
-            monkeypatch.delenv("RT_NO_DEDUP", raising=False)
+        ctx_opts(dedup_triangles=0 if mode == "all" else 1)
         gpu_ctx.upload(rtlib.Scene.builtin(scene, images=[img], meshes=[m]))
         gpu_ctx.render_init(W, H, 1984)
         fb = torch.zeros(nfb * H * W * 3, dtype=torch.float32, device="cuda")
@@ -511,10 +509,10 @@ def test_host_buffers_match_device(rtlib, gpu_ctx, oracle):
 
 
 @pytest.mark.parametrize("threshold", ["0", "6", "1e9"], ids=["lists", "default", "traverse"])
-def test_camera_lists_on_and_off(rtlib, gpu_ctx, oracle, threshold, monkeypatch):
+def test_camera_lists_on_and_off(rtlib, gpu_ctx, oracle, threshold, ctx_opts):
     """Camera rays through the 8x8-tile candidate lists (threshold 0), the product's default
     threshold (6 items per resident lane: off for this size) and never: same bits as the oracle."""
-    monkeypatch.setenv("RT_BINS_MIN_ITEMS_PER_LANE", threshold)
+    ctx_opts(bins_min_items_per_lane=float(threshold))
     W, H, spp, nfb = 96, 54, 2, 2
     gpu, rows, cnt, _, _ = _gpu_render(rtlib, gpu_ctx, "big1", W, H, spp, 0, nfb, REF)
     ref = oracle.RefScene("big1")
@@ -529,18 +527,18 @@ def test_camera_lists_on_and_off(rtlib, gpu_ctx, oracle, threshold, monkeypatch)
 @pytest.mark.parametrize("order", [None, "0"], ids=["longest_first", "item_order"])
 @pytest.mark.parametrize("min_segs", [None, "1"], ids=["default", "every_item"])
 @pytest.mark.parametrize("band", [None, (4, 1, 3)], ids=["full", "share"])
-def test_split_samples_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch, min_segs, band, order):
+def test_split_samples_bit_exact(rtlib, gpu_ctx, oracle, ctx_opts, min_segs, band, order):
     """Warm launches split the samples of the longest items over work items (launch 1 measures,
     launch 2 records the sample-start RNG states and segment counts, launches 3+ claim the split
-    samples and the other items longest first -- or, RT_SPLIT_ORDER=0, samples in item order -- and
+    samples and the other items longest first -- or, options.split_order = 0, samples in item order -- and
     merge): every launch's frame buffer equals the oracle's bit for bit, with the same segment and
     sample counts."""
     import torch
 
     if min_segs:
-        monkeypatch.setenv("RT_SPLIT_MIN_SEGMENTS", min_segs)
+        ctx_opts(split_min_segments=float(min_segs))
     if order is not None:
-        monkeypatch.setenv("RT_SPLIT_ORDER", order)
+        ctx_opts(split_order=int(order))
     W, H, spp, nfb = 96, 54, 4, 2
     sc = rtlib.Scene.builtin("big1")
     gpu_ctx.upload(sc)  # new scene generation: a fresh schedule

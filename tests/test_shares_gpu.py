@@ -7,7 +7,7 @@ curand_init(1984, slot, 0), render.h:91,101 -- so every owned row must equal the
 row bit for bit, on the cold launch and on the scheduled (longest-first) launches that follow it.
 Share-size dependent paths exercised here: the camera-ray entry masks of list worlds
 (bin_masks_kernel), the item schedule of a small share, and the step kernel's camera-list threshold
-(RT_BINS_MIN_ITEMS_PER_LANE) on both sides of its switch.
+(options.bins_min_items_per_lane) on both sides of its switch.
 """
 import os
 
@@ -103,14 +103,11 @@ def test_c5_share_full_size(rtlib, gpu_ctx, oracle, n, rank):
 
 @pytest.mark.parametrize("threshold", [None, "0", "1e9"], ids=["default", "lists", "traverse"])
 @pytest.mark.parametrize("n", [4, 8])
-def test_step_share_across_camera_list_switch(rtlib, gpu_ctx, oracle, monkeypatch, n, threshold):
+def test_step_share_across_camera_list_switch(rtlib, gpu_ctx, oracle, ctx_opts, n, threshold):
     """C2's 10-fb workload as rank N-1 of N = 4 (9.2 items per resident lane: camera lists on at the
     product's threshold of 6) and N = 8 (4.6: off), 1 spp per fb; also forced on and off.  Cold and
     scheduled launches against the oracle on an owned-row subset."""
-    if threshold is None:
-        monkeypatch.delenv("RT_BINS_MIN_ITEMS_PER_LANE", raising=False)
-    else:
-        monkeypatch.setenv("RT_BINS_MIN_ITEMS_PER_LANE", threshold)
+    ctx_opts(bins_min_items_per_lane=6.0 if threshold is None else float(threshold))
     W, H, spp, nfb = 1200, 800, 1, 10
     rank = n - 1
     gpu_ctx.upload(rtlib.Scene.builtin("big1"))
@@ -126,11 +123,11 @@ def test_step_share_across_camera_list_switch(rtlib, gpu_ctx, oracle, monkeypatc
 
 
 @pytest.mark.parametrize("scene", ["cornell", "cornell_smoke", "earth", "two_perlin", "final"])
-def test_world_tree_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch, scene):
-    """The opt-in world tree (RT_WORLD_TREE=1 at upload: a list world flattened into one traversal tree
+def test_world_tree_bit_exact(rtlib, gpu_ctx, oracle, ctx_opts, scene):
+    """The opt-in world tree (options.world_tree = 1 at upload: a list world flattened into one traversal tree
     for render_step_kernel, media after it in list order, inert sphere-bounded media skipped for sane
     rays): bit-exact against the oracle, full frame and a share, cold and scheduled launches."""
-    monkeypatch.setenv("RT_WORLD_TREE", "1")
+    ctx_opts(world_tree=1)
     pa, oa = _assets(scene, (341, 152))
     if scene == "earth":
         from raytracing_gpu_amd import assets
@@ -211,14 +208,14 @@ def test_multi_rccl_one_rank_matches_draw(rtlib):
 @pytest.mark.parametrize("min_segs", [None, "1"], ids=["default", "every_item"])
 @pytest.mark.parametrize("band", [None, (4, 1, 3)], ids=["full", "share"])
 @pytest.mark.parametrize("scene", ["cornell_smoke", "final"])
-def test_list_world_split_samples_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch, scene, band, min_segs, cam):
+def test_list_world_split_samples_bit_exact(rtlib, gpu_ctx, oracle, ctx_opts, scene, band, min_segs, cam):
     """Split samples in render_kernel's parking variants (C5's F_FINAL; cornell_smoke through the
     widest global-memory variant F_ALL, as C3's own narrow variant does not split): launch 1 measures, launch 2
     records the sample-start RNG states of the longest items, launches 3+ run their samples as separate
     work items and merge them in sample order.  Every launch equals the oracle bit for bit, in both
     camera modes, full frame and share, at the product's threshold and with every item split."""
     if min_segs:
-        monkeypatch.setenv("RT_SPLIT_MIN_SEGMENTS", min_segs)
+        ctx_opts(split_min_segments=float(min_segs))
     pa, oa = _assets(scene, (341, 152))
     W, H, spp, nfb = (96, 54, 4, 2) if scene == "final" else (48, 48, 4, 2)
     gpu_ctx.upload(rtlib.Scene.builtin(scene, **pa))  # a new scene generation: a fresh schedule
@@ -247,17 +244,15 @@ def test_list_world_split_samples_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch,
 
 @pytest.mark.parametrize("mode", ["merged", "fallback", "entry_loop"])
 @pytest.mark.parametrize("scene", ["final", "first", "two_perlin", "cornell"])
-def test_merged_list_search_bit_exact(rtlib, gpu_ctx, oracle, monkeypatch, scene, mode):
+def test_merged_list_search_bit_exact(rtlib, gpu_ctx, oracle, ctx_opts, scene, mode):
     """render_kernel's merged list-world search (world_search: every entry's candidates in one
     winner/second pair with list tie keys, one settle per query; scenes of primitives, BVHs, instances
     and inert media): C5's own variant on final, the widest global-memory variant F_ALL on the
-    primitive-only lists.  "fallback" (RT_MERGE_FALLBACK) runs the search and then answers every query
-    through the exact entry loop, "entry_loop" (RT_NO_MERGE) is the per-entry world_hit.  Full frame and
+    primitive-only lists.  "fallback" (RT_MERGE_FALLBACK_ALL) runs the search and then answers every
+    query through the exact entry loop, "entry_loop" (RT_MERGE_OFF) is the per-entry world_hit.  Full frame and
     a share, cold and scheduled launches, against the oracle bit for bit."""
-    if mode == "fallback":
-        monkeypatch.setenv("RT_MERGE_FALLBACK", "1")
-    elif mode == "entry_loop":
-        monkeypatch.setenv("RT_NO_MERGE", "1")
+    ctx_opts(merged_search={"merged": rtlib.RT_MERGE_ON, "fallback": rtlib.RT_MERGE_FALLBACK_ALL,
+                            "entry_loop": rtlib.RT_MERGE_OFF}[mode])
     pa, oa = _assets(scene, (341, 152))
     W, H, spp, nfb = (96, 54, 2, 2) if scene != "cornell" else (48, 48, 4, 2)
     gpu_ctx.upload(rtlib.Scene.builtin(scene, **pa))  # merge_ok is decided at upload
