@@ -67,6 +67,7 @@ enum : int {
   F_WORLD = 1 << 15,  // list world flattened into ONE traversal tree (render_step_kernel; rt_scene_upload)
   F_QLDS = 1 << 16,   // the world BVH's traversal tree quantized to 24-byte pair records in LDS (qpair)
   F_MERGE = 1 << 17,  // render_kernel answers world queries with world_search only (merge_ok scenes)
+  F_COOP = 1 << 18,   // render_step_kernel with the cooperative tail search (coop_search; cold launches)
   F_ALL = (1 << 11) - 2,
   F_SPHERES = F_MOVING | F_CHECKER | F_BVH,           // basic, first, big1 (C2), two_spheres
   F_CORNELL = F_RECT | F_LIST | F_XFORM | F_MEDIUM,   // cornell, cornell_smoke (C3)
@@ -116,6 +117,10 @@ struct DScene {
   const uint32_t* qnodes;
   int32_t q_pairs;
   int32_t q_ebias;
+  // Leaves of the world BVH's traversal tree (primitive ids; coincident triangles deduplicated), for
+  // the cooperative tail search of render_step_kernel (coop_search)
+  const int32_t* coop_leaf;
+  int32_t n_coop_leaf;
   rt_camera cam;
   float bg[3];
 };
@@ -924,6 +929,61 @@ __device__ __forceinline__ void tile_candidates(const DScene& S, const int32_t* 
   }
 }
 
+// Cooperative tail search (render_step_kernel, worlds whose first entry is one BVH).  Once the work
+// counter is exhausted a wave's traversing lanes are the launch's last items, and a lane's segment
+// is a chain of ~14 dependent traversal steps whatever the other 63 lanes do.  A wave holding few
+// such lanes answers their queries one at a time with all 64 lanes instead: lane k tests the leaves
+// k, k + 64, ... of the world BVH's traversal tree (coop_leaf: every primitive a traversal can reach),
+// then the per-lane candidates are combined across the wave.  The combined state is what
+// take_candidate would hold after seeing every leaf in some order with nothing culled, so bvh_settle
+// decides it as after a traversal: the winner is the candidate with the smallest lo (ties: the lower
+// reference rank), `second` the smallest lo of the others (an exact loser of an exact winner left
+// out, as take_candidate does), and a query that is not certain re-runs on the exact visit set.
+struct Cand {
+  float lo, hi, sec;
+  int prim, rank;
+};
+__device__ __forceinline__ void coop_merge(Cand& a, const Cand& b) {
+  const bool exact2 = a.lo == a.hi && b.lo == b.hi;
+  const bool bw = b.lo < a.lo || (b.lo == a.lo && b.rank < a.rank);
+  const float lost = bw ? a.lo : b.lo;
+  a.sec = __builtin_fminf(a.sec, b.sec);
+  if (!exact2) a.sec = __builtin_fminf(a.sec, lost);
+  if (bw) {
+    a.lo = b.lo;
+    a.hi = b.hi;
+    a.prim = b.prim;
+    a.rank = b.rank;
+  }
+}
+template <int F>
+__device__ __forceinline__ Cand coop_search(const DScene& S, int L, const Ray& rl, float tmin, float tmax,
+                                            unsigned& nprim) {
+  // lane L's ray, wave-uniform from here on
+  auto bc = [L](float x) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), L)); };
+  Ray r;
+  r.o = mk(bc(rl.o.x), bc(rl.o.y), bc(rl.o.z));
+  r.d = mk(bc(rl.d.x), bc(rl.d.y), bc(rl.d.z));
+  r.tm = bc(rl.tm);
+  const float a = len2(r.d), rcpa = __builtin_amdgcn_rcpf(a);  // the query setup's own operations
+  Cand c{__builtin_inff(), __builtin_inff(), __builtin_inff(), -1, 0x7fffffff};
+  const int n = S.n_coop_leaf;
+  for (int q = (int)__lane_id(); q < n; q += 64) {
+    const int pi = S.coop_leaf[q];
+    const PrimRec rec = load_prim<F>(S, pi);
+    float lo, hi;
+    if (prim_range<F>(S, rec, r, a, rcpa, tmin, tmax, lo, hi, nprim))
+      take_candidate(lo, hi, pi, __float_as_int(rec.c.y), c.lo, c.hi, c.sec, c.prim, c.rank);
+  }
+  #pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {  // butterfly: every lane ends with the wave's combined state
+    const Cand o{__shfl_xor(c.lo, m, 64), __shfl_xor(c.hi, m, 64), __shfl_xor(c.sec, m, 64),
+                 __shfl_xor(c.prim, m, 64), __shfl_xor(c.rank, m, 64)};
+    coop_merge(c, o);
+  }
+  return c;
+}
+
 // Reference-chain validation of a candidate search's winner (best_prim at exact t = best, reference
 // leaf rank best_rank of the BVH at `base` with `rows` inner levels): true when the reference's
 // visit set certainly reaches it, i.e. every reference ancestor passes the slab test against
@@ -1699,7 +1759,8 @@ struct RenderParams {
   long long npix;  // W*H of the full image
   int W, H, rows, spp, fb_first, max_depth, cam_mode, fb_count;
   int shade_min;  // render_step_kernel: lanes waiting before a wave runs its shading phase
-  int pad4;
+  int coop_max;   // render_step_kernel: once the work counter is exhausted, waves with at most this many
+                  // traversing lanes answer their queries cooperatively (coop_search); 0 = never
   // Item schedule (see rt_render): perm maps the claimed position to the item (null: identity);
   // positions below n_long hold the longest items of the previous launch, longest first, and the
   // waves holding one run at raised priority.  item_cost (measuring launch) receives each item's
@@ -2437,6 +2498,29 @@ void render_step_kernel(const RenderParams P) {
     }
     RT_STAMP(3);
     if (__ballot(mode != 0) == 0) break;  // no item left for any lane of the wave (mode 2: a listed camera ray)
+    // ---- the launch's tail: few traversing lanes, no item left to claim -> cooperative searches
+    if constexpr ((F & F_COOP) != 0) {
+      if (__ballot(done) != 0) {  // a lane's claim failed: the counter is exhausted
+        unsigned long long t = __ballot(mode == 1);
+        if (t != 0 && __popcll(t) <= P.coop_max) {
+          do {
+            const int L = __ffsll((long long)t) - 1;
+            t &= t - 1;
+            const Cand c = coop_search<F>(S, L, ray, tmin, tmax, nprim);
+            if ((int)lane == L) {
+              best = c.lo;
+              bhi = c.hi;
+              second = c.sec;
+              best_prim = c.prim;
+              best_rank = c.rank;
+              overflow = false;
+              mode = 2;
+            }
+          } while (t != 0);
+          continue;  // to the shading phase
+        }
+      }
+    }
     // ---- traversal steps until shade_min lanes wait (or none traverses)
     for (;;) {
       RT_STEP_COUNT(3);
@@ -2912,6 +2996,8 @@ const Variant kVariants[] = {
     RT_VARIANT_STEP(F_SPHERES | F_STEP),
     RT_VARIANT_STEP(F_MESH | F_STEP),
     RT_VARIANT_STEP(F_MESH | F_STEP | F_QLDS),
+    RT_VARIANT_STEP(F_SPHERES | F_LDS | F_STEP | F_COOP),
+    RT_VARIANT_STEP(F_MESH | F_STEP | F_QLDS | F_COOP),
     RT_VARIANT_STEP(F_CORNELL | F_WORLD | F_STEP),
     RT_VARIANT_STEP(F_FINAL | F_WORLD | F_STEP),
     RT_VARIANT(F_SPHERES),
@@ -2943,8 +3029,8 @@ constexpr int kLdsBudget = 156 * 1024;  // bytes of staged nodes + primitives + 
 
 // Smallest compiled variant that covers the scene's features and the requested mode.
 int pick_variant(int features, bool stats, bool exact, bool check, bool lds, bool widest = false, bool step = false,
-                 bool world = false, bool qlds = false, bool merge = false) {
-  const int modes = F_STATS | F_EXACT | F_CHECK | F_LDS | F_STEP | F_WORLD | F_QLDS | F_MERGE;
+                 bool world = false, bool qlds = false, bool merge = false, bool coop = false) {
+  const int modes = F_STATS | F_EXACT | F_CHECK | F_LDS | F_STEP | F_WORLD | F_QLDS | F_MERGE | F_COOP;
   const int mode = check ? F_CHECK : ((stats ? F_STATS : 0) | (exact ? F_EXACT : 0));
   auto best_of = [&](int want) {  // covering variant with the fewest (widest: most) feature bits
     int best = -1;
@@ -2969,7 +3055,13 @@ int pick_variant(int features, bool stats, bool exact, bool check, bool lds, boo
       if (kVariants[w].mask == (kVariants[v].mask | F_STEP | (world ? F_WORLD : 0))) sv = w;
     if (sv >= 0 && qlds)  // ... with its traversal tree quantized in LDS
       for (int w = 0; w < kNumVariants; ++w)
-        if (kVariants[w].mask == (kVariants[sv].mask | F_QLDS)) return w;
+        if (kVariants[w].mask == (kVariants[sv].mask | F_QLDS)) {
+          sv = w;
+          break;
+        }
+    if (sv >= 0 && coop)  // ... with the cooperative tail search
+      for (int w = 0; w < kNumVariants; ++w)
+        if (kVariants[w].mask == (kVariants[sv].mask | F_COOP)) return w;
     if (sv >= 0) return sv;
   }
   if (v >= 0 && merge && mode == 0)  // its merged-search twin (render_kernel; merge_ok scenes)
@@ -3127,7 +3219,8 @@ struct SahBuilder {
 };
 
 int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<rt_prim>& prims,
-                         std::vector<rt_bvh_node>& nodes, std::vector<float2>& pmargin, int* n_pairs, bool dedup) {
+                         std::vector<rt_bvh_node>& nodes, std::vector<float2>& pmargin, int* n_pairs, bool dedup,
+                         std::vector<int32_t>* leaves_out) {
   const int inner = (1 << rows) - 1, last0 = (1 << (rows - 1)) - 1;
   std::vector<int> members;
   for (int k = last0; k < inner; ++k) {
@@ -3200,6 +3293,7 @@ int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<
   SahBuilder sb{box, nodes, fb};
   sb.build(leaves.data(), (int)leaves.size(), 0);
   *n_pairs = (int)leaves.size() - 1;  // records of the tree (one per inner node): leaves - 1
+  if (leaves_out) leaves_out->assign(leaves.begin(), leaves.end());
   return fb;
 }
 
@@ -3481,6 +3575,7 @@ void rt_ctx_options_default(rt_ctx_options* o) {
   o->split_order = 1;
   o->cost_shift = -1;
   o->long_pct = 2.0f;
+  o->coop_max = 0;
 }
 
 int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
@@ -3488,7 +3583,7 @@ int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
   if (o->merged_search < RT_MERGE_ON || o->merged_search > RT_MERGE_FALLBACK_ALL ||
       o->merge_order < RT_ORDER_DISTANCE || o->merge_order > RT_ORDER_REVERSED || o->shade_min < 0 ||
       o->shade_min > 64 || !(o->bins_min_items_per_lane >= 0.0f) || !(o->split_min_segments >= 0.0f) ||
-      o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f))
+      o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f) || o->coop_max < 0 || o->coop_max > 64)
     return fail(c, RT_ERR_ARG, "bad context options");
   c->opt = *o;
   // the schedule and split thresholds come from the options: every configuration starts cold again
@@ -3832,12 +3927,14 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   std::vector<rt_object> objects(s->objects, s->objects + s->n_objects);
   std::vector<float2> pmargin(s->n_prims, make_float2(-INFINITY, -INFINITY));
   std::vector<int> tree_pairs(objects.size(), 0);  // records of each BVH object's traversal tree
+  std::vector<int32_t> coop_leaf;                  // leaves of the world[0] BVH's tree (coop_search)
   for (size_t k = 0; k < objects.size(); ++k) {
     rt_object& o = objects[k];
     o.c = -1;
     if (o.kind == RT_OBJ_MEDIUM && medium_inert(s, o)) o.c = 1;  // object_query skips it for sane rays
     if (o.kind == RT_OBJ_BVH) {
-      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes, pmargin, &tree_pairs[k], c->opt.dedup_triangles != 0);
+      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes, pmargin, &tree_pairs[k], c->opt.dedup_triangles != 0,
+                                            (int)k == s->world[0] ? &coop_leaf : nullptr);
       if (fast < 0) return fail(c, RT_ERR_SCENE, "malformed reference bvh");
       o.c = fast;
     }
@@ -3941,6 +4038,8 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
     std::stable_sort(worder.begin(), worder.end(), [&](int x, int y) { return key[(size_t)x] < key[(size_t)y]; });
   }
   if ((rc = upload(c, worder.data(), worder.size(), &d.worder))) return rc;
+  if (world_step && (rc = upload(c, coop_leaf.data(), coop_leaf.size(), &d.coop_leaf))) return rc;
+  d.n_coop_leaf = world_step ? (int)coop_leaf.size() : 0;
   if (q_pairs > 0 && (rc = upload(c, qnodes.data(), qnodes.size(), &d.qnodes))) return rc;
   d.q_pairs = q_pairs;
   d.q_ebias = q_ebias;
@@ -4174,12 +4273,17 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   const bool use_lds = lds_bytes + 1024 * kStackDepth * 2 <= (size_t)kLdsBudget && c->dev_nodes / 2 < 32768 &&
                        c->dev_prims < 32768 && (a->flags & RT_FLAG_NO_LDS) == 0;
   const bool step = (c->world_step || c->world_tree) && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
-  const bool qlds = !use_lds && c->scene.q_pairs > 0 && (a->flags & RT_FLAG_NO_LDS) == 0;
+  // (the quantized tree applies to the variants that have a QLDS twin, whether or not the whole scene
+  // would fit the LDS image of the F_LDS variants: no triangle-mesh variant has an F_LDS twin)
+  const bool qlds = c->scene.q_pairs > 0 && (a->flags & RT_FLAG_NO_LDS) == 0;
   // the variants that stage their materials and textures after the locker (tables_after_locker) need
   // them to fit: a list world without BVHs whose tables exceed 32 KB runs the widest variant instead
   const bool big_tables = (size_t)16 * ((size_t)c->dev_mats + 2 * (size_t)c->dev_texs) > 32768;
+  // cold launches (nothing known of the items' lengths: the launch ends with whatever long items
+  // started last) run the stepwise variant with the cooperative tail search, when it is enabled
+  const bool coop = c->opt.coop_max > 0 && !have_perm && c->scene.n_coop_leaf > 0 && !c->world_tree;
   int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
-                         (a->flags & RT_FLAG_WIDEST) != 0, step, c->world_tree, qlds, c->scene.merge_ok != 0);
+                         (a->flags & RT_FLAG_WIDEST) != 0, step, c->world_tree, qlds, c->scene.merge_ok != 0, coop);
   if (var >= 0 && big_tables && (kVariants[var].mask & (F_LDS | F_QLDS | F_STEP | F_BVH | F_TRI)) == 0)
     var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds, true, step,
                        c->world_tree, qlds, c->scene.merge_ok != 0);
@@ -4282,6 +4386,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   }
   P.item_cost = (sched && !have_perm) ? c->item_cost : nullptr;
   if (c->opt.shade_min > 0) P.shade_min = c->opt.shade_min;
+  P.coop_max = c->opt.coop_max;
   if (check) {
     if (!c->dbg) {
       HIPCHK(c, hipMalloc((void**)&c->dbg, 16 * sizeof(float) * kAuditCap + 64));

@@ -6,7 +6,8 @@
 #   tests            pytest -m gpu (TESTS="-k expr" narrows it)
 #   smoke            __graft_entry__.smoke()
 #   c2 c2x100 c3 c3full c4 c5 c5full   bench.py lines of the BASELINE configs (C2 = the default)
-#   scale_c2 scale_c4 scale_c5         scripts/diag_scale.py: every rank's share on this GPU
+#   scale_c2 scale_c2x100 scale_c4 scale_c5   scripts/diag_scale.py: every rank's share on this GPU
+#                                      (SCALE_OPTS="--opt coop_max=8" passes context options)
 #   prof             scripts/prof_all.sh: rocprofv3 kernel traces + PMC passes of C2-C5
 #   isa              scripts/isa_meta.py (registers / spills of every instantiation)
 # BENCH_ARGS is appended to every bench line (e.g. BENCH_ARGS="--opt shade_min=52").
@@ -43,9 +44,10 @@ for s in ${STEPS:-tests smoke c2}; do
     c4) bench c4 $C4 --no-cpu-baseline ;;
     c5) bench c5 $C5 --no-cpu-baseline ;;
     c5full) bench c5full --scene final --width 3840 --height 2159 --spp 100 --nfb 100 --steps 1 --warmup 0 --cold-steps 1 --no-cpu-baseline --no-stats ;;
-    scale_c2) run scale_c2 600 python -u scripts/diag_scale.py || exit $? ;;
-    scale_c4) run scale_c4 600 python -u scripts/diag_scale.py door 1920 1079 16 16 || exit $? ;;
-    scale_c5) run scale_c5 600 python -u scripts/diag_scale.py final 3840 2159 4 4 || exit $? ;;
+    scale_c2) run scale_c2 600 python -u scripts/diag_scale.py big1 1200 800 10 10 ${SCALE_OPTS:-} || exit $? ;;
+    scale_c4) run scale_c4 600 python -u scripts/diag_scale.py door 1920 1079 16 16 ${SCALE_OPTS:-} || exit $? ;;
+    scale_c5) run scale_c5 600 python -u scripts/diag_scale.py final 3840 2159 4 4 ${SCALE_OPTS:-} || exit $? ;;
+    scale_c2x100) run scale_c2x100 600 python -u scripts/diag_scale.py big1 1200 800 100 1 ${SCALE_OPTS:-} || exit $? ;;
     prof) STEP_TIMEOUT=300 bash scripts/prof_all.sh || exit $? ;;
     isa) run isa 300 python scripts/isa_meta.py gpurun_out/isa_meta.txt || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
