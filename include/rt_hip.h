@@ -249,9 +249,7 @@ typedef struct rt_ctx_options {
   int32_t cost_shift;        /* item-schedule cost buckets of 2^cost_shift segments; -1 = automatic */
   float long_pct;            /* share of the longest items whose waves run at raised priority
                                 (default 2)                                                         */
-  int32_t coop_max;          /* stepwise kernel: once the work counter is exhausted, a wave with at
-                                most this many traversing lanes answers their queries with all 64
-                                lanes (cooperative tail search); 0 = never                          */
+  int32_t pad;
 } rt_ctx_options;
 void rt_ctx_options_default(rt_ctx_options* opts);
 int rt_ctx_set_options(rt_ctx* ctx, const rt_ctx_options* opts);

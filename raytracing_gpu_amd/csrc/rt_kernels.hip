@@ -67,7 +67,6 @@ enum : int {
   F_WORLD = 1 << 15,  // list world flattened into ONE traversal tree (render_step_kernel; rt_scene_upload)
   F_QLDS = 1 << 16,   // the world BVH's traversal tree quantized to 24-byte pair records in LDS (qpair)
   F_MERGE = 1 << 17,  // render_kernel answers world queries with world_search only (merge_ok scenes)
-  F_COOP = 1 << 18,   // render_step_kernel with the cooperative tail search (coop_search; cold launches)
   F_ALL = (1 << 11) - 2,
   F_SPHERES = F_MOVING | F_CHECKER | F_BVH,           // basic, first, big1 (C2), two_spheres
   F_CORNELL = F_RECT | F_LIST | F_XFORM | F_MEDIUM,   // cornell, cornell_smoke (C3)
@@ -94,7 +93,9 @@ struct DScene {
   unsigned* dbg_n;
   int32_t dbg_cap;
   int32_t n_world;
-  int32_t lds_nodes;     // F_LDS: node count staged (the primitives follow them)
+  int32_t lds_nodes;     // F_LDS: node slots staged (the primitives follow them)
+  int32_t lds_fb;        // F_LDS|F_STEP: first node of the world BVH's traversal tree, staged in planes
+  int32_t lds_pairs;     // ... and its pair records (<= kPlanePairs)
   int32_t lds_prims;     // F_LDS: primitive count staged (validation margins follow them)
   int32_t lds_mats;      // F_LDS: materials staged after the margins (one float4 each)
   int32_t lds_texs;      // F_LDS: textures staged after the materials (two float4 each; stacks follow)
@@ -117,10 +118,6 @@ struct DScene {
   const uint32_t* qnodes;
   int32_t q_pairs;
   int32_t q_ebias;
-  // Leaves of the world BVH's traversal tree (primitive ids; coincident triangles deduplicated), for
-  // the cooperative tail search of render_step_kernel (coop_search)
-  const int32_t* coop_leaf;
-  int32_t n_coop_leaf;
   rt_camera cam;
   float bg[3];
 };
@@ -184,12 +181,15 @@ __device__ __forceinline__ int lds_mats_at(const DScene& S) {
 __host__ __device__ __forceinline__ int qlds_mats_at(const DScene& S) {
   return ((6 * S.q_pairs + 1024 * kStackDepthQ / 2) + 3) / 4;  // float4 index, 16-byte aligned
 }
-// render_kernel's variants without BVHs or triangles (C3) stage them after their locker too.
+// render_kernel's variants without BVHs or triangles (C3) stage them after their locker too, and so does
+// the merged-search variant (C5): its stacks and locker leave 1 KB of a quarter CU's LDS, room for a
+// scene's tables (materials, textures, images) of up to 1 KB (rt_render checks; else the entry-loop
+// variant runs).
 constexpr int stack_words(int mask);
 constexpr int locker_words(int mask);
 template <int F>
 constexpr bool tables_after_locker() {
-  return (F & (F_LDS | F_QLDS | F_STEP | F_BVH | F_TRI)) == 0;
+  return (F & (F_LDS | F_QLDS | F_STEP | F_BVH | F_TRI)) == 0 || (F & F_MERGE) != 0;
 }
 template <int F>
 constexpr int locker_tables_at() {  // float4 index after the stacks and the locker (256-thread blocks)
@@ -212,6 +212,8 @@ __device__ __forceinline__ const rt_texture* texs_of(const DScene& S) {
 template <int F>
 __device__ __forceinline__ const rt_image* imgs_of(const DScene& S) {
   if constexpr ((F & F_QLDS) != 0) return (const rt_image*)(rt_lds + qlds_mats_at(S) + S.lds_mats + 2 * S.lds_texs);
+  else if constexpr (tables_after_locker<F>())
+    return (const rt_image*)(rt_lds + locker_tables_at<F>() + S.lds_mats + 2 * S.lds_texs);
   else return S.images;
 }
 // Stack entries: child words (pair index, or -1 - primitive).  F_LDS scenes have < 32768 pairs and
@@ -274,12 +276,31 @@ __device__ __forceinline__ uint32_t* locker_of() {
   return (uint32_t*)rt_lds + render_block<F>() * stack_words(F) + threadIdx.x;
 }
 
+// The stepwise LDS variant stages the world BVH's traversal tree (node slots lds_fb ..) in four planes
+// of kPlanePairs float4 each -- plane c holds float4 c of every 64-byte pair record -- instead of
+// record after record: the four ds_read_b128 of a traversal step then read 16-byte slots (pair mod 16)
+// of the 256-byte bank row instead of 4 slots (pair mod 4), so a 16-lane group's reads spread over all
+// 64 banks (MI355X_MICROARCH.md, LDS), at the same address arithmetic (plane offsets are immediates).
+constexpr int kPlanePairs = 512;
+template <int F>
+constexpr bool planes() {
+  return (F & F_LDS) != 0 && (F & F_STEP) != 0;
+}
 // Stage the read-only scene arrays a F_LDS variant reads in LDS, once per workgroup.
 template <int F>
 __device__ __forceinline__ void stage_lds(const DScene& S) {
   constexpr int BS = render_block<F>();
   const int nn = 2 * S.lds_nodes, np = 3 * S.lds_prims, nm = (S.lds_prims + 1) / 2;
-  for (int q = threadIdx.x; q < nn; q += BS) rt_lds[q] = S.nodes[q];
+  if constexpr (planes<F>()) {
+    const int nf = 2 * S.lds_fb;  // reference trees as they are, then the traversal tree in planes
+    for (int q = threadIdx.x; q < nf; q += BS) rt_lds[q] = S.nodes[q];
+    for (int q = threadIdx.x; q < 4 * kPlanePairs; q += BS) {
+      const int c = q / kPlanePairs, k = q - c * kPlanePairs;
+      rt_lds[nf + q] = k < S.lds_pairs ? S.nodes[nf + 4 * k + c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+  } else {
+    for (int q = threadIdx.x; q < nn; q += BS) rt_lds[q] = S.nodes[q];
+  }
   for (int q = threadIdx.x; q < np; q += BS) rt_lds[nn + q] = S.prims[q];
   const float4* pm = (const float4*)S.pmargin;  // padded to an even count at upload
   for (int q = threadIdx.x; q < nm; q += BS) rt_lds[nn + np + q] = pm[q];
@@ -824,8 +845,20 @@ __device__ __forceinline__ bool trav_step(const DScene& S, int fb, const Ray& r,
   if constexpr ((F & F_QLDS) != 0) {
     qpair(S, cur, oi, finv, tmin, cut, hl, hr, tl, tr, c0, c1);
   } else {
-    const float4* n = nodes_of<F>(S) + 2 * (fb + 2 * cur);
-    const float4 l0 = n[0], l1 = n[1], r0 = n[2], r1 = n[3];
+    float4 l0, l1, r0, r1;
+    if constexpr (planes<F>()) {  // the four planes of the staged tree (stage_lds)
+      const float4* n = nodes_of<F>(S) + 2 * fb + cur;
+      l0 = n[0];
+      l1 = n[kPlanePairs];
+      r0 = n[2 * kPlanePairs];
+      r1 = n[3 * kPlanePairs];
+    } else {
+      const float4* n = nodes_of<F>(S) + 2 * (fb + 2 * cur);
+      l0 = n[0];
+      l1 = n[1];
+      r0 = n[2];
+      r1 = n[3];
+    }
     hl = fbox(l0, l1, oi, finv, tmin, cut, tl);
     hr = fbox(r0, r1, oi, finv, tmin, cut, tr);
     c0 = __float_as_int(l0.w);
@@ -927,61 +960,6 @@ __device__ __forceinline__ void tile_candidates(const DScene& S, const int32_t* 
       }
     }
   }
-}
-
-// Cooperative tail search (render_step_kernel, worlds whose first entry is one BVH).  Once the work
-// counter is exhausted a wave's traversing lanes are the launch's last items, and a lane's segment
-// is a chain of ~14 dependent traversal steps whatever the other 63 lanes do.  A wave holding few
-// such lanes answers their queries one at a time with all 64 lanes instead: lane k tests the leaves
-// k, k + 64, ... of the world BVH's traversal tree (coop_leaf: every primitive a traversal can reach),
-// then the per-lane candidates are combined across the wave.  The combined state is what
-// take_candidate would hold after seeing every leaf in some order with nothing culled, so bvh_settle
-// decides it as after a traversal: the winner is the candidate with the smallest lo (ties: the lower
-// reference rank), `second` the smallest lo of the others (an exact loser of an exact winner left
-// out, as take_candidate does), and a query that is not certain re-runs on the exact visit set.
-struct Cand {
-  float lo, hi, sec;
-  int prim, rank;
-};
-__device__ __forceinline__ void coop_merge(Cand& a, const Cand& b) {
-  const bool exact2 = a.lo == a.hi && b.lo == b.hi;
-  const bool bw = b.lo < a.lo || (b.lo == a.lo && b.rank < a.rank);
-  const float lost = bw ? a.lo : b.lo;
-  a.sec = __builtin_fminf(a.sec, b.sec);
-  if (!exact2) a.sec = __builtin_fminf(a.sec, lost);
-  if (bw) {
-    a.lo = b.lo;
-    a.hi = b.hi;
-    a.prim = b.prim;
-    a.rank = b.rank;
-  }
-}
-template <int F>
-__device__ __forceinline__ Cand coop_search(const DScene& S, int L, const Ray& rl, float tmin, float tmax,
-                                            unsigned& nprim) {
-  // lane L's ray, wave-uniform from here on
-  auto bc = [L](float x) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), L)); };
-  Ray r;
-  r.o = mk(bc(rl.o.x), bc(rl.o.y), bc(rl.o.z));
-  r.d = mk(bc(rl.d.x), bc(rl.d.y), bc(rl.d.z));
-  r.tm = bc(rl.tm);
-  const float a = len2(r.d), rcpa = __builtin_amdgcn_rcpf(a);  // the query setup's own operations
-  Cand c{__builtin_inff(), __builtin_inff(), __builtin_inff(), -1, 0x7fffffff};
-  const int n = S.n_coop_leaf;
-  for (int q = (int)__lane_id(); q < n; q += 64) {
-    const int pi = S.coop_leaf[q];
-    const PrimRec rec = load_prim<F>(S, pi);
-    float lo, hi;
-    if (prim_range<F>(S, rec, r, a, rcpa, tmin, tmax, lo, hi, nprim))
-      take_candidate(lo, hi, pi, __float_as_int(rec.c.y), c.lo, c.hi, c.sec, c.prim, c.rank);
-  }
-  #pragma unroll
-  for (int m = 1; m < 64; m <<= 1) {  // butterfly: every lane ends with the wave's combined state
-    const Cand o{__shfl_xor(c.lo, m, 64), __shfl_xor(c.hi, m, 64), __shfl_xor(c.sec, m, 64),
-                 __shfl_xor(c.prim, m, 64), __shfl_xor(c.rank, m, 64)};
-    coop_merge(c, o);
-  }
-  return c;
 }
 
 // Reference-chain validation of a candidate search's winner (best_prim at exact t = best, reference
@@ -1662,8 +1640,9 @@ __device__ __forceinline__ V tex_leaf(const DScene& S, const rt_texture& T, floa
       int j = (int)(vv * (double)im.height);
       if (i >= im.width) i = im.width - 1;
       if (j >= im.height) j = im.height - 1;
-      const uint8_t* px =
-          S.texels + im.offset + (size_t)j * im.width * im.bytes_per_pixel + (size_t)i * im.bytes_per_pixel;
+      // texel (i, j) in the tiled copy rt_scene_upload made: 8x8-texel tiles, row-major
+      const unsigned t = ((unsigned)((j >> 3) * ((im.width + 7) >> 3) + (i >> 3)) << 6) + ((j & 7) << 3) + (i & 7);
+      const uint8_t* px = S.texels + im.offset + (size_t)t * im.bytes_per_pixel;
       const float cs = 1.0f / 255.0f;
       return mk(cs * (float)px[0], cs * (float)px[1], cs * (float)px[2]);
     }
@@ -1759,8 +1738,7 @@ struct RenderParams {
   long long npix;  // W*H of the full image
   int W, H, rows, spp, fb_first, max_depth, cam_mode, fb_count;
   int shade_min;  // render_step_kernel: lanes waiting before a wave runs its shading phase
-  int coop_max;   // render_step_kernel: once the work counter is exhausted, waves with at most this many
-                  // traversing lanes answer their queries cooperatively (coop_search); 0 = never
+  int pad4;
   // Item schedule (see rt_render): perm maps the claimed position to the item (null: identity);
   // positions below n_long hold the longest items of the previous launch, longest first, and the
   // waves holding one run at raised priority.  item_cost (measuring launch) receives each item's
@@ -1887,11 +1865,13 @@ __global__ __launch_bounds__(render_block<F>()) __attribute__((amdgpu_waves_per_
 void render_kernel(const RenderParams P) {
   const DScene& S = P.S;
   if constexpr ((F & F_LDS) != 0) stage_lds<F>(S);  // nodes, primitives, margins, materials, textures
-  if constexpr (tables_after_locker<F>()) {  // materials and textures after the locker
+  if constexpr (tables_after_locker<F>()) {  // materials, textures and images after the locker
     static_assert(render_block<F>() == 256, "locker_tables_at assumes 256-thread blocks");
     float4* m = rt_lds + locker_tables_at<F>();
-    const int nm = S.lds_mats, nt = 2 * S.lds_texs;
-    for (int k = threadIdx.x; k < nm + nt; k += 256) m[k] = k < nm ? ((const float4*)S.mats)[k] : ((const float4*)S.texs)[k - nm];
+    const int nm = S.lds_mats, nt = 2 * S.lds_texs, ni = S.lds_imgs;
+    for (int k = threadIdx.x; k < nm + nt + ni; k += 256)
+      m[k] = k < nm ? ((const float4*)S.mats)[k]
+                    : (k < nm + nt ? ((const float4*)S.texs)[k - nm] : ((const float4*)S.images)[k - nm - nt]);
     __syncthreads();
   }
   const unsigned lane = __lane_id();
@@ -2498,29 +2478,6 @@ void render_step_kernel(const RenderParams P) {
     }
     RT_STAMP(3);
     if (__ballot(mode != 0) == 0) break;  // no item left for any lane of the wave (mode 2: a listed camera ray)
-    // ---- the launch's tail: few traversing lanes, no item left to claim -> cooperative searches
-    if constexpr ((F & F_COOP) != 0) {
-      if (__ballot(done) != 0) {  // a lane's claim failed: the counter is exhausted
-        unsigned long long t = __ballot(mode == 1);
-        if (t != 0 && __popcll(t) <= P.coop_max) {
-          do {
-            const int L = __ffsll((long long)t) - 1;
-            t &= t - 1;
-            const Cand c = coop_search<F>(S, L, ray, tmin, tmax, nprim);
-            if ((int)lane == L) {
-              best = c.lo;
-              bhi = c.hi;
-              second = c.sec;
-              best_prim = c.prim;
-              best_rank = c.rank;
-              overflow = false;
-              mode = 2;
-            }
-          } while (t != 0);
-          continue;  // to the shading phase
-        }
-      }
-    }
     // ---- traversal steps until shade_min lanes wait (or none traverses)
     for (;;) {
       RT_STEP_COUNT(3);
@@ -2963,6 +2920,7 @@ struct rt_ctx {
   bool world_step = false;  // one BVH object followed by primitive objects (render_step_kernel applies)
   bool world_tree = false;  // a list world flattened into the world tree (render_step_kernel<..|F_WORLD>)
   int dev_nodes = 0, dev_prims = 0, dev_mats = 0, dev_texs = 0, dev_imgs = 0;  // device array sizes (LDS staging)
+  int plane_fb = -1, plane_pairs = 0;  // world tree staged in planes by the stepwise LDS variant (-1: not)
   float last_ms = 0.0f;
   int last_sched = 0;  // RT_SCHED_* of the last render launch
   char last_kernel[48] = "";  // rocprof name stem of the last render launch, e.g. render_step_kernel<25730>
@@ -2996,8 +2954,6 @@ const Variant kVariants[] = {
     RT_VARIANT_STEP(F_SPHERES | F_STEP),
     RT_VARIANT_STEP(F_MESH | F_STEP),
     RT_VARIANT_STEP(F_MESH | F_STEP | F_QLDS),
-    RT_VARIANT_STEP(F_SPHERES | F_LDS | F_STEP | F_COOP),
-    RT_VARIANT_STEP(F_MESH | F_STEP | F_QLDS | F_COOP),
     RT_VARIANT_STEP(F_CORNELL | F_WORLD | F_STEP),
     RT_VARIANT_STEP(F_FINAL | F_WORLD | F_STEP),
     RT_VARIANT(F_SPHERES),
@@ -3029,8 +2985,8 @@ constexpr int kLdsBudget = 156 * 1024;  // bytes of staged nodes + primitives + 
 
 // Smallest compiled variant that covers the scene's features and the requested mode.
 int pick_variant(int features, bool stats, bool exact, bool check, bool lds, bool widest = false, bool step = false,
-                 bool world = false, bool qlds = false, bool merge = false, bool coop = false) {
-  const int modes = F_STATS | F_EXACT | F_CHECK | F_LDS | F_STEP | F_WORLD | F_QLDS | F_MERGE | F_COOP;
+                 bool world = false, bool qlds = false, bool merge = false) {
+  const int modes = F_STATS | F_EXACT | F_CHECK | F_LDS | F_STEP | F_WORLD | F_QLDS | F_MERGE;
   const int mode = check ? F_CHECK : ((stats ? F_STATS : 0) | (exact ? F_EXACT : 0));
   auto best_of = [&](int want) {  // covering variant with the fewest (widest: most) feature bits
     int best = -1;
@@ -3055,13 +3011,7 @@ int pick_variant(int features, bool stats, bool exact, bool check, bool lds, boo
       if (kVariants[w].mask == (kVariants[v].mask | F_STEP | (world ? F_WORLD : 0))) sv = w;
     if (sv >= 0 && qlds)  // ... with its traversal tree quantized in LDS
       for (int w = 0; w < kNumVariants; ++w)
-        if (kVariants[w].mask == (kVariants[sv].mask | F_QLDS)) {
-          sv = w;
-          break;
-        }
-    if (sv >= 0 && coop)  // ... with the cooperative tail search
-      for (int w = 0; w < kNumVariants; ++w)
-        if (kVariants[w].mask == (kVariants[sv].mask | F_COOP)) return w;
+        if (kVariants[w].mask == (kVariants[sv].mask | F_QLDS)) return w;
     if (sv >= 0) return sv;
   }
   if (v >= 0 && merge && mode == 0)  // its merged-search twin (render_kernel; merge_ok scenes)
@@ -3219,8 +3169,7 @@ struct SahBuilder {
 };
 
 int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<rt_prim>& prims,
-                         std::vector<rt_bvh_node>& nodes, std::vector<float2>& pmargin, int* n_pairs, bool dedup,
-                         std::vector<int32_t>* leaves_out) {
+                         std::vector<rt_bvh_node>& nodes, std::vector<float2>& pmargin, int* n_pairs, bool dedup) {
   const int inner = (1 << rows) - 1, last0 = (1 << (rows - 1)) - 1;
   std::vector<int> members;
   for (int k = last0; k < inner; ++k) {
@@ -3293,7 +3242,6 @@ int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<
   SahBuilder sb{box, nodes, fb};
   sb.build(leaves.data(), (int)leaves.size(), 0);
   *n_pairs = (int)leaves.size() - 1;  // records of the tree (one per inner node): leaves - 1
-  if (leaves_out) leaves_out->assign(leaves.begin(), leaves.end());
   return fb;
 }
 
@@ -3575,7 +3523,6 @@ void rt_ctx_options_default(rt_ctx_options* o) {
   o->split_order = 1;
   o->cost_shift = -1;
   o->long_pct = 2.0f;
-  o->coop_max = 0;
 }
 
 int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
@@ -3583,7 +3530,7 @@ int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
   if (o->merged_search < RT_MERGE_ON || o->merged_search > RT_MERGE_FALLBACK_ALL ||
       o->merge_order < RT_ORDER_DISTANCE || o->merge_order > RT_ORDER_REVERSED || o->shade_min < 0 ||
       o->shade_min > 64 || !(o->bins_min_items_per_lane >= 0.0f) || !(o->split_min_segments >= 0.0f) ||
-      o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f) || o->coop_max < 0 || o->coop_max > 64)
+      o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f))
     return fail(c, RT_ERR_ARG, "bad context options");
   c->opt = *o;
   // the schedule and split thresholds come from the options: every configuration starts cold again
@@ -3927,14 +3874,12 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   std::vector<rt_object> objects(s->objects, s->objects + s->n_objects);
   std::vector<float2> pmargin(s->n_prims, make_float2(-INFINITY, -INFINITY));
   std::vector<int> tree_pairs(objects.size(), 0);  // records of each BVH object's traversal tree
-  std::vector<int32_t> coop_leaf;                  // leaves of the world[0] BVH's tree (coop_search)
   for (size_t k = 0; k < objects.size(); ++k) {
     rt_object& o = objects[k];
     o.c = -1;
     if (o.kind == RT_OBJ_MEDIUM && medium_inert(s, o)) o.c = 1;  // object_query skips it for sane rays
     if (o.kind == RT_OBJ_BVH) {
-      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes, pmargin, &tree_pairs[k], c->opt.dedup_triangles != 0,
-                                            (int)k == s->world[0] ? &coop_leaf : nullptr);
+      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes, pmargin, &tree_pairs[k], c->opt.dedup_triangles != 0);
       if (fast < 0) return fail(c, RT_ERR_SCENE, "malformed reference bvh");
       o.c = fast;
     }
@@ -3989,8 +3934,29 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   if ((rc = upload(c, pmargin.data(), pmargin.size(), &d.pmargin))) return rc;
   if ((rc = upload(c, s->textures, (size_t)s->n_textures, &d.texs))) return rc;
   if ((rc = upload(c, s->perlins, (size_t)s->n_perlins, &d.perlins))) return rc;
-  if ((rc = upload(c, s->images, (size_t)s->n_images, &d.images))) return rc;
-  if ((rc = upload(c, s->texels, (size_t)s->n_texels, &d.texels))) return rc;
+  // Image textures in 8x8-texel tiles (row-major tiles, row-major texels inside a tile): a texel's 2-D
+  // neighbours share its cache lines, whichever way the texture's axes run across the image.  The
+  // device image records point into the tiled copy; texel values are unchanged.
+  std::vector<rt_image> dimages(s->images, s->images + s->n_images);
+  std::vector<uint8_t> dtexels;
+  for (rt_image& im : dimages) {
+    if (im.width <= 0) continue;  // no data: the cyan fallback (texture.h:146-147)
+    const long long n = (long long)im.width * im.height * im.bytes_per_pixel;
+    if (im.height <= 0 || im.bytes_per_pixel < 1 || im.bytes_per_pixel > 4 || im.offset < 0 || im.offset + n > s->n_texels)
+      return fail(c, RT_ERR_SCENE, "image texels out of range");
+    if (dtexels.size() + ((size_t)n * 2) >= (size_t)1 << 31) return fail(c, RT_ERR_SCENE, "textures too large");
+    const uint8_t* src = s->texels + im.offset;
+    const int bpp = im.bytes_per_pixel, tpr = (im.width + 7) >> 3, tpc = (im.height + 7) >> 3;
+    const size_t base = dtexels.size();
+    dtexels.resize(base + (size_t)tpr * tpc * 64 * bpp, 0);
+    for (int j = 0; j < im.height; ++j)
+      for (int i = 0; i < im.width; ++i)
+        memcpy(&dtexels[base + (((size_t)((j >> 3) * tpr + (i >> 3)) << 6) + ((j & 7) << 3) + (i & 7)) * bpp],
+               src + ((size_t)j * im.width + i) * bpp, (size_t)bpp);
+    im.offset = (int32_t)base;
+  }
+  if ((rc = upload(c, dimages.data(), dimages.size(), &d.images))) return rc;
+  if ((rc = upload(c, dtexels.data(), dtexels.size(), &d.texels))) return rc;
   if ((rc = upload(c, wleaf.data(), wleaf.size(), &d.wleaf))) return rc;
   if ((rc = upload(c, wxf.data(), wxf.size(), &d.wxf))) return rc;
   d.wt_fb = wt_fb;
@@ -4038,8 +4004,6 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
     std::stable_sort(worder.begin(), worder.end(), [&](int x, int y) { return key[(size_t)x] < key[(size_t)y]; });
   }
   if ((rc = upload(c, worder.data(), worder.size(), &d.worder))) return rc;
-  if (world_step && (rc = upload(c, coop_leaf.data(), coop_leaf.size(), &d.coop_leaf))) return rc;
-  d.n_coop_leaf = world_step ? (int)coop_leaf.size() : 0;
   if (q_pairs > 0 && (rc = upload(c, qnodes.data(), qnodes.size(), &d.qnodes))) return rc;
   d.q_pairs = q_pairs;
   d.q_ebias = q_ebias;
@@ -4085,6 +4049,17 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
     c->bin_n = -(int)sph.size();  // negative: entry spheres (masks), not primitive spheres (lists)
   }
   c->dev_nodes = (int)nodes.size();
+  // the stepwise LDS variant stages the world BVH's traversal tree in planes (stage_lds): it must be
+  // the last tree of the node array and have at most kPlanePairs records
+  c->plane_fb = -1;
+  if (world_step) {
+    const rt_object& wo = objects[(size_t)s->world[0]];
+    const int np = tree_pairs[(size_t)s->world[0]];
+    if (np >= 1 && np <= kPlanePairs && wo.c + 2 * np == (int)nodes.size()) {
+      c->plane_fb = wo.c;
+      c->plane_pairs = np;
+    }
+  }
   c->dev_prims = (int)prims.size();
   c->dev_mats = s->n_materials;
   c->dev_imgs = s->n_images;
@@ -4268,22 +4243,25 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
 
   const bool stats = a->stats != 0;
   const bool check = (a->flags & RT_FLAG_AUDIT) != 0;
-  const size_t lds_bytes =
-      (size_t)(2 * c->dev_nodes + 3 * c->dev_prims + (c->dev_prims + 1) / 2 + c->dev_mats + 2 * c->dev_texs) * sizeof(float4);
-  const bool use_lds = lds_bytes + 1024 * kStackDepth * 2 <= (size_t)kLdsBudget && c->dev_nodes / 2 < 32768 &&
-                       c->dev_prims < 32768 && (a->flags & RT_FLAG_NO_LDS) == 0;
   const bool step = (c->world_step || c->world_tree) && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
+  // node slots of the LDS image: the stepwise variant's world tree in planes of kPlanePairs records
+  const int lds_node_slots = step && c->world_step ? (c->plane_fb >= 0 ? c->plane_fb + 2 * kPlanePairs : -1) : c->dev_nodes;
+  const size_t lds_bytes =
+      (size_t)(2 * lds_node_slots + 3 * c->dev_prims + (c->dev_prims + 1) / 2 + c->dev_mats + 2 * c->dev_texs) * sizeof(float4);
+  const bool use_lds = lds_node_slots >= 0 && lds_bytes + 1024 * kStackDepth * 2 <= (size_t)kLdsBudget &&
+                       c->dev_nodes / 2 < 32768 && c->dev_prims < 32768 && (a->flags & RT_FLAG_NO_LDS) == 0;
   // (the quantized tree applies to the variants that have a QLDS twin, whether or not the whole scene
   // would fit the LDS image of the F_LDS variants: no triangle-mesh variant has an F_LDS twin)
   const bool qlds = c->scene.q_pairs > 0 && (a->flags & RT_FLAG_NO_LDS) == 0;
-  // the variants that stage their materials and textures after the locker (tables_after_locker) need
-  // them to fit: a list world without BVHs whose tables exceed 32 KB runs the widest variant instead
-  const bool big_tables = (size_t)16 * ((size_t)c->dev_mats + 2 * (size_t)c->dev_texs) > 32768;
-  // cold launches (nothing known of the items' lengths: the launch ends with whatever long items
-  // started last) run the stepwise variant with the cooperative tail search, when it is enabled
-  const bool coop = c->opt.coop_max > 0 && !have_perm && c->scene.n_coop_leaf > 0 && !c->world_tree;
+  // the variants that stage their materials, textures and images after the locker (tables_after_locker)
+  // need them to fit: a list world without BVHs whose tables exceed 32 KB runs the widest variant
+  // instead, a merged-search scene whose tables exceed 1 KB the entry-loop variant
+  const size_t table_bytes = (size_t)16 * ((size_t)c->dev_mats + 2 * (size_t)c->dev_texs + (size_t)c->dev_imgs);
+  const bool big_tables = table_bytes > 32768;
+  const bool merge_tables_fit = table_bytes <= 1024;
   int var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds,
-                         (a->flags & RT_FLAG_WIDEST) != 0, step, c->world_tree, qlds, c->scene.merge_ok != 0, coop);
+                         (a->flags & RT_FLAG_WIDEST) != 0, step, c->world_tree, qlds,
+                         c->scene.merge_ok != 0 && merge_tables_fit);
   if (var >= 0 && big_tables && (kVariants[var].mask & (F_LDS | F_QLDS | F_STEP | F_BVH | F_TRI)) == 0)
     var = pick_variant(c->features, stats, (a->flags & RT_FLAG_EXACT_TRAVERSAL) != 0, check, use_lds, true, step,
                        c->world_tree, qlds, c->scene.merge_ok != 0);
@@ -4386,7 +4364,6 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   }
   P.item_cost = (sched && !have_perm) ? c->item_cost : nullptr;
   if (c->opt.shade_min > 0) P.shade_min = c->opt.shade_min;
-  P.coop_max = c->opt.coop_max;
   if (check) {
     if (!c->dbg) {
       HIPCHK(c, hipMalloc((void**)&c->dbg, 16 * sizeof(float) * kAuditCap + 64));
@@ -4398,19 +4375,24 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   }
   const int bs = variant_block(var);
   const bool lds_var = (kVariants[var].mask & F_LDS) != 0;
-  P.S.lds_nodes = lds_var ? c->dev_nodes : 0;
+  const bool planes_var = lds_var && (kVariants[var].mask & F_STEP) != 0;
+  if (planes_var && (c->plane_fb < 0 || lds_node_slots != c->plane_fb + 2 * kPlanePairs))
+    return fail(c, RT_ERR_STATE, "stepwise LDS variant without a plane-staged world tree");
+  P.S.lds_nodes = lds_var ? (planes_var ? lds_node_slots : c->dev_nodes) : 0;
+  P.S.lds_fb = planes_var ? c->plane_fb : 0;
+  P.S.lds_pairs = planes_var ? c->plane_pairs : 0;
   P.S.lds_prims = lds_var ? c->dev_prims : 0;
   const bool qlds_var = (kVariants[var].mask & F_QLDS) != 0;
   const int vmask = kVariants[var].mask;
-  const bool tables_var = (vmask & (F_LDS | F_QLDS | F_STEP | F_BVH | F_TRI)) == 0;
+  const bool tables_var = (vmask & (F_LDS | F_QLDS | F_STEP | F_BVH | F_TRI)) == 0 || (vmask & F_MERGE) != 0;
   P.S.lds_mats = (lds_var || qlds_var || tables_var) ? c->dev_mats : 0;
   P.S.lds_texs = (lds_var || qlds_var || tables_var) ? c->dev_texs : 0;
-  P.S.lds_imgs = qlds_var ? c->dev_imgs : 0;
+  P.S.lds_imgs = (qlds_var || tables_var) ? c->dev_imgs : 0;
   static_assert(kStackDepthQ == kStackDepth, "F_QLDS stacks");
   const size_t shmem = lds_var    ? lds_bytes + (size_t)bs * kStackDepth * 2
                        : qlds_var ? (size_t)16 * (qlds_mats_at(P.S) + c->dev_mats + 2 * c->dev_texs + c->dev_imgs)
                                   : (size_t)bs * (stack_words(vmask) + locker_words(vmask)) * 4 +
-                                        (tables_var ? (size_t)16 * (c->dev_mats + 2 * c->dev_texs) : 0);
+                                        (tables_var ? table_bytes : 0);
   // Camera-ray culling, built once per (scene, W, H): candidate lists for the stepwise kernel
   // (world = one BVH), top-level entry masks for list worlds.  Not in the exact / audit modes,
   // whose counters are the reference's.

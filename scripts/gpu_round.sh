@@ -3,11 +3,11 @@
 # limit; stops at the first crash-like exit (timeout, abort, segfault) and at a failed test run.
 #   STEPS="tests c2 c4 scale_c4" bash scripts/gpu_round.sh
 # Steps:
-#   tests            pytest -m gpu (TESTS="-k expr" narrows it)
+#   tests            pytest -m gpu (TESTS_K="expr" narrows it to pytest -k expr)
 #   smoke            __graft_entry__.smoke()
 #   c2 c2x100 c3 c3full c4 c5 c5full   bench.py lines of the BASELINE configs (C2 = the default)
 #   scale_c2 scale_c2x100 scale_c4 scale_c5   scripts/diag_scale.py: every rank's share on this GPU
-#                                      (SCALE_OPTS="--opt coop_max=8" passes context options)
+#                                      (SCALE_OPTS="--opt KEY=VALUE" passes context options)
 #   prof             scripts/prof_all.sh: rocprofv3 kernel traces + PMC passes of C2-C5
 #   isa              scripts/isa_meta.py (registers / spills of every instantiation)
 # BENCH_ARGS is appended to every bench line (e.g. BENCH_ARGS="--opt shade_min=52").
@@ -35,7 +35,7 @@ C4="--scene door --width 1920 --height 1079 --spp 16 --nfb 16"
 C5="--scene final --width 3840 --height 2159 --spp 4 --nfb 4"
 for s in ${STEPS:-tests smoke c2}; do
   case $s in
-    tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TESTS:-} || exit $? ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TESTS_K:+-k "$TESTS_K"} || exit $? ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     c2) bench c2 ;;
     c2x100) bench c2x100 --nfb 1 --spp 100 --no-cpu-baseline ;;
