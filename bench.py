@@ -289,7 +289,8 @@ def main():
     kw = dict(band_rows=a.band_rows, band_first=rank, band_stride=world, exact=a.exact, lds=not a.no_lds,
               step=not a.no_step, bins=not a.no_bins)
     args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, schedule=not a.no_schedule, **kw)
-    cold_args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, schedule=False, **kw)
+    cold_args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, schedule=not a.no_schedule,
+                             fresh=True, **kw)
     rows = rt.owned_rows(args)
     all_rows = []
     for r in range(world):
@@ -336,13 +337,14 @@ def main():
     tiny = rt.make_args(64, 36, 1, 0, 1, a.depth, cam)
     tfb = torch.empty(64 * 36 * 3, dtype=torch.float32, device=dev)
     ctx.render(tiny, tfb.data_ptr())
-    # cold draws: nothing reused from an earlier launch (RT_FLAG_NO_SCHEDULE), as one draw() runs
+    # cold draws: nothing reused from an earlier launch (RT_FLAG_FRESH: each runs as the first draw
+    # of its configuration does -- probe launch, schedule from its estimate, render)
     step(cold_args)
     kms.clear()
     sched.clear()
     dt_cold = timed(max(1, a.cold_steps), cold_args) / max(1, a.cold_steps)
     cold_kms = sum(kms) / len(kms)
-    assert all(x == 0 for x in sched), sched
+    assert all(x & (rt.RT_SCHED_PREVIOUS | rt.RT_SCHED_SPLIT_REPLAY) == 0 for x in sched), sched
     cold_sched = sorted(set(sched))
 
     stats = None
@@ -376,7 +378,8 @@ def main():
                  "context_options": opts or "defaults",
                  "schedule": "steady state: every timed draw repeats the configuration and reuses the item "
                              "schedule (and split-sample states) of the draws before it; cold_* = draws that "
-                             "reuse nothing (RT_FLAG_NO_SCHEDULE), as a single draw() runs",
+                             "reuse nothing (RT_FLAG_FRESH), as a single draw() runs: probe launch, "
+                             "schedule from its estimate, render (bit 4 = probe-scheduled)",
                  "timed_schedule_bits": sorted(set(sched)), "cold_schedule_bits": cold_sched,
                  "driver": "torch.distributed (one process per GPU)" if world > 1 else "single process"}
         out = out_line(a, value, world, dt / a.steps, segs, roof, extra)
@@ -420,7 +423,8 @@ def main_inprocess(a):
     cam = rt.RT_CAM_REF_SLOT0 if a.cam == "ref" else rt.RT_CAM_PER_PIXEL
     kw = dict(band_rows=a.band_rows, exact=a.exact, lds=not a.no_lds, step=not a.no_step, bins=not a.no_bins)
     args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, schedule=not a.no_schedule, **kw)
-    cold_args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, schedule=False, **kw)
+    cold_args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, schedule=not a.no_schedule,
+                             fresh=True, **kw)
     m.draw(rt.make_args(64, 36, 1, 0, 1, a.depth, cam, band_rows=4))  # module load on every device
     m.draw(cold_args)
     colds = []
@@ -448,7 +452,8 @@ def main_inprocess(a):
              "gather_bytes": warm[-1]["gather_bytes"], "warm": warm[-1]["warm"],
              "schedule": "steady state: every timed draw repeats the configuration and reuses the item "
                          "schedule (and split-sample states) of the draws before it; cold_* = draws that "
-                         "reuse nothing (RT_FLAG_NO_SCHEDULE), as a single draw() runs",
+                         "reuse nothing (RT_FLAG_FRESH), as a single draw() runs: probe launch, "
+                         "schedule from its estimate, render",
              "driver": f"librt_multi.so in one process, {a.gpus} ranks on devices {devices}, "
                        f"gather {'ncclGather (RCCL)' if mode == multi.RT_GATHER_RCCL else 'host copies'}; "
                        "a step includes the copy of the assembled image to the host"}

@@ -178,6 +178,9 @@ enum rt_cam_mode {
                                      tile's candidate list (world = one BVH; same pixels)       */
 #define RT_FLAG_NO_SPLIT 128      /* never split the samples of the longest items over work items
                                      on warm launches (stepwise kernel; same pixels)            */
+#define RT_FLAG_FRESH 256         /* forget the context's item schedule first: the launch runs as
+                                     the first launch of its configuration does (benchmarks of a
+                                     one-shot draw; same pixels)                                */
 
 typedef struct rt_render_args {
   int32_t width, height;  /* full image size; N = width*height drives the RNG slots (H3)  */
@@ -249,7 +252,10 @@ typedef struct rt_ctx_options {
   int32_t cost_shift;        /* item-schedule cost buckets of 2^cost_shift segments; -1 = automatic */
   float long_pct;            /* share of the longest items whose waves run at raised priority
                                 (default 2)                                                         */
-  int32_t pad;
+  int32_t probe_schedule;    /* 1: the first launch of a configuration of >= 4 samples per pixel
+                                claims its items longest first by a probe launch's estimate (one
+                                sample of the first fb per pixel, output discarded); 0: natural
+                                order (default 1)                                                   */
 } rt_ctx_options;
 void rt_ctx_options_default(rt_ctx_options* opts);
 int rt_ctx_set_options(rt_ctx* ctx, const rt_ctx_options* opts);
@@ -283,6 +289,8 @@ const char* rt_last_render_kernel(const rt_ctx* ctx);
                                    launch of this configuration (same scene, size, spp, depth, fb
                                    range, tiling and camera mode)                               */
 #define RT_SCHED_SPLIT_REPLAY 2 /* split samples started from RNG states an earlier launch recorded */
+#define RT_SCHED_PROBE 4        /* items claimed longest first by a probe launch's estimate (the
+                                   first launch of a configuration, options.probe_schedule)     */
 int32_t rt_last_render_schedule(const rt_ctx* ctx);
 /* Audit log of the last RT_FLAG_AUDIT render: 16 floats per disagreeing BVH query (ray o[3] d[3]
  * time, tmin, tmax, culled t, culled prim (int bits), exact t, exact prim, culled rank, 0, 0).

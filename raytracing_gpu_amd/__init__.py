@@ -36,8 +36,10 @@ RT_FLAG_NO_STEP = 16
 RT_FLAG_NO_SCHEDULE = 32
 RT_FLAG_NO_CAMERA_BINS = 64
 RT_FLAG_NO_SPLIT = 128
+RT_FLAG_FRESH = 256
 RT_SCHED_PREVIOUS = 1
 RT_SCHED_SPLIT_REPLAY = 2
+RT_SCHED_PROBE = 4
 
 PRIM_SPHERE, PRIM_MOVING_SPHERE, PRIM_RECT_XY, PRIM_RECT_XZ, PRIM_RECT_YZ, PRIM_TRIANGLE = range(6)
 OBJ_PRIM, OBJ_LIST, OBJ_BVH, OBJ_XFORM, OBJ_MEDIUM = range(5)
@@ -101,7 +103,7 @@ class rt_ctx_options(ctypes.Structure):
     _fields_ = [("world_tree", c_int32), ("quantized_tree", c_int32), ("merged_search", c_int32),
                 ("merge_order", c_int32), ("dedup_triangles", c_int32), ("shade_min", c_int32),
                 ("bins_min_items_per_lane", c_float), ("split_min_segments", c_float), ("split_order", c_int32),
-                ("cost_shift", c_int32), ("long_pct", c_float), ("pad", c_int32)]
+                ("cost_shift", c_int32), ("long_pct", c_float), ("probe_schedule", c_int32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
@@ -275,13 +277,14 @@ def make_args(width: int, height: int, spp: int, fb_first: int = 0, fb_count: in
               cam_mode: int = RT_CAM_REF_SLOT0, band_rows: int = 0, band_first: int = 0, band_stride: int = 1,
               stats: bool = False, seed: int = 1984, exact: bool = False, audit: bool = False,
               lds: bool = True, widest: bool = False, step: bool = True, schedule: bool = True,
-              bins: bool = True, split: bool = True) -> rt_render_args:
+              bins: bool = True, split: bool = True, fresh: bool = False) -> rt_render_args:
     flags = (RT_FLAG_EXACT_TRAVERSAL if exact else 0) | (RT_FLAG_AUDIT if audit else 0) | (0 if lds else RT_FLAG_NO_LDS)
     flags |= RT_FLAG_WIDEST if widest else 0
     flags |= 0 if step else RT_FLAG_NO_STEP
     flags |= 0 if schedule else RT_FLAG_NO_SCHEDULE
     flags |= 0 if bins else RT_FLAG_NO_CAMERA_BINS
     flags |= 0 if split else RT_FLAG_NO_SPLIT
+    flags |= RT_FLAG_FRESH if fresh else 0
     return rt_render_args(width, height, spp, fb_first, fb_count, max_depth, cam_mode,
                           band_rows if band_rows > 0 else height, band_first, band_stride,
                           1 if stats else 0, flags, seed)

@@ -89,6 +89,7 @@ struct DScene {
   const rt_image* images;
   const uint8_t* texels;
   const float2* pmargin; // per prim: reference-chain safety margins (see bvh_closest)
+  const float4* pvalid;  // per prim, 3 float4: the chain check in one fetch (chain_ok's first test)
   float* dbg;            // audit log (F_CHECK): 16 floats per disagreeing BVH query
   unsigned* dbg_n;
   int32_t dbg_cap;
@@ -978,6 +979,28 @@ __device__ __forceinline__ bool chain_ok(const DScene& S, int base, int rows, co
   const float dmax = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.d.x), __builtin_fabsf(r.d.y)),
                                      __builtin_fabsf(r.d.z));
   const float bound = 0.001953125f * best * dmax;  // 2^-9 * t * |d|_inf
+  if constexpr ((F & (F_LDS | F_MEDIUM)) == 0 && (F & F_TRI) != 0) {
+    // The loop below in one 48-byte fetch, in global-memory mesh variants, where every ancestor node
+    // is an L2 round trip (C4 door: the loop's dependent fetches were ~19 % of a launch).  It comes
+    // first there: 0.7 % faster on C4 than after the sphere test.  Not in C3's rect variant (no gain
+    // measured) nor in C5's, which spills (0.6 % slower).  pvalid = {box of the LOWEST position of the
+    // `must` set below, mask}, {its hi, safe}, {largest |coordinate| over the `must` boxes}.  Those boxes contain the lowest one
+    // (checked at upload), so the computed hit point is at least as deep inside each as inside the
+    // lowest, and each one's margin `need` (below) is at most the record's: a hit point deeper than that
+    // inside the lowest one passes the loop's test at every position -- the loop's own answer, true.
+    const float4 v0 = S.pvalid[3 * best_prim], v1 = S.pvalid[3 * best_prim + 1], v2 = S.pvalid[3 * best_prim + 2];
+    if (bound < v1.w) {  // the loop's `must` is the mask (else every position is tested)
+      if (__float_as_uint(v0.w) == 0u) return true;
+      const V p = r.o + best * r.d;
+      const float dx = __builtin_fminf(p.x - v0.x, v1.x - p.x);
+      const float dy = __builtin_fminf(p.y - v0.y, v1.y - p.y);
+      const float dz = __builtin_fminf(p.z - v0.z, v1.z - p.z);
+      const float need_max = 0x1p-20f * (v2.x + 2.0f * (__builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(r.o.x),
+                                                                                      __builtin_fabsf(r.o.y)),
+                                                                       __builtin_fabsf(r.o.z)) + best * dmax));
+      if (__builtin_fminf(__builtin_fminf(dx, dy), dz) > need_max) return true;
+    }
+  }
   {
     // Every reference ancestor contains the winner's box, so a computed hit point deeper inside
     // the winner's own box than `bound` passes all of them: a sphere touches its box only at
@@ -2880,6 +2903,8 @@ struct rt_ctx {
   // Item schedule of the last configuration (scene generation, size, spp, depth, fb range, tiling):
   // per-item segment counts of its measuring launch -> longest items first (perm).
   uint16_t* item_cost = nullptr;
+  uint16_t* probe_cost = nullptr;  // per (owned row, pixel): the probe launch's segment counts
+  long long probe_cap = 0;
   uint32_t* perm = nullptr;
   long long item_cap = 0;
   static constexpr int kKey = 11;
@@ -3169,7 +3194,8 @@ struct SahBuilder {
 };
 
 int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<rt_prim>& prims,
-                         std::vector<rt_bvh_node>& nodes, std::vector<float2>& pmargin, int* n_pairs, bool dedup) {
+                         std::vector<rt_bvh_node>& nodes, std::vector<float2>& pmargin, std::vector<float4>& pvalid,
+                         int* n_pairs, bool dedup) {
   const int inner = (1 << rows) - 1, last0 = (1 << (rows - 1)) - 1;
   std::vector<int> members;
   for (int k = last0; k < inner; ++k) {
@@ -3210,6 +3236,28 @@ int build_traversal_tree(const rt_scene_soa* s, int base, int rows, std::vector<
       float mbits;
       memcpy(&mbits, &mask, 4);
       pmargin[id] = make_float2(mbits, safe);
+      // chain_ok's one-fetch record: the lowest `must` position's box, the mask, `safe`, and the largest
+      // |coordinate| over the `must` ancestors' boxes.  Only when every `must` ancestor contains the
+      // lowest one's box (the reference's surrounding boxes always do); else safe = -inf turns it off.
+      int low = k;  // node of the lowest must position
+      for (int q = 0; mask != 0u && q < __builtin_ctz(mask); ++q) low = (low - 1) >> 1;
+      const rt_bvh_node& ln = s->nodes[base + low];
+      float rmax = 0.0f, vsafe = safe;
+      pos = 0;
+      for (int a = k;; a = (a - 1) >> 1, ++pos) {
+        if ((mask >> pos) & 1u) {
+          const rt_bvh_node& an = s->nodes[base + a];
+          for (int q = 0; q < 3; ++q) {
+            rmax = std::fmax(rmax, std::fmax(std::fabs(an.lo[q]), std::fabs(an.hi[q])));
+            if (!(an.lo[q] <= ln.lo[q] && an.hi[q] >= ln.hi[q])) vsafe = -INFINITY;
+          }
+        }
+        if (a == 0) break;
+      }
+      if (!(rmax < INFINITY)) vsafe = -INFINITY;
+      pvalid[3 * (size_t)id] = make_float4(ln.lo[0], ln.lo[1], ln.lo[2], mbits);
+      pvalid[3 * (size_t)id + 1] = make_float4(ln.hi[0], ln.hi[1], ln.hi[2], vsafe);
+      pvalid[3 * (size_t)id + 2] = make_float4(rmax, 0.0f, 0.0f, 0.0f);
     }
   }
   // Coincident triangles (the reference's mesh import indexes the concatenated vertex array with
@@ -3312,6 +3360,20 @@ int sort_scatter(rt_ctx* c, long long n, const unsigned* base, uint32_t* out) {
   order_scatter_kernel<<<tiles, 64, 0, c->stream>>>(c->sort_scratch, (unsigned long long)n, tile_tab, base, out);
   HIPCHK(c, hipGetLastError());
   return RT_OK;
+}
+
+// Probe estimate of every item: its pixel's probe count (sample 0 of the first fb) times spp.  Items
+// are row-major with the fb inside the row (render kernels); the probe launch's items are (row, pixel).
+__global__ __launch_bounds__(kBlock) void probe_expand_kernel(const uint16_t* __restrict__ probe,
+                                                              uint16_t* __restrict__ cost, unsigned long long items,
+                                                              int W, int fbc, int spp) {
+  const unsigned long long per_row = (unsigned long long)fbc * (unsigned)W;
+  for (unsigned long long k = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; k < items;
+       k += (unsigned long long)gridDim.x * blockDim.x) {
+    const unsigned long long q = k / per_row, i = (k - q * per_row) % (unsigned)W;
+    const unsigned v = (unsigned)probe[q * (unsigned)W + i] * (unsigned)spp;
+    cost[k] = (uint16_t)(v < 65535u ? v : 65535u);
+  }
 }
 
 // Item schedule of a configuration from its measuring launch's per-item segment counts (c->item_cost,
@@ -3490,6 +3552,7 @@ int rt_ctx_destroy(rt_ctx* c) {
   if (c->row_map) (void)hipFree(c->row_map);
   if (c->row_cost) (void)hipFree(c->row_cost);
   if (c->item_cost) (void)hipFree(c->item_cost);
+  if (c->probe_cost) (void)hipFree(c->probe_cost);
   if (c->perm) (void)hipFree(c->perm);
   if (c->dbg) (void)hipFree(c->dbg);
   if (c->tiles) (void)hipFree(c->tiles);
@@ -3523,6 +3586,7 @@ void rt_ctx_options_default(rt_ctx_options* o) {
   o->split_order = 1;
   o->cost_shift = -1;
   o->long_pct = 2.0f;
+  o->probe_schedule = 1;
 }
 
 int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
@@ -3530,7 +3594,8 @@ int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
   if (o->merged_search < RT_MERGE_ON || o->merged_search > RT_MERGE_FALLBACK_ALL ||
       o->merge_order < RT_ORDER_DISTANCE || o->merge_order > RT_ORDER_REVERSED || o->shade_min < 0 ||
       o->shade_min > 64 || !(o->bins_min_items_per_lane >= 0.0f) || !(o->split_min_segments >= 0.0f) ||
-      o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f))
+      o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f) || o->probe_schedule < 0 ||
+      o->probe_schedule > 1)
     return fail(c, RT_ERR_ARG, "bad context options");
   c->opt = *o;
   // the schedule and split thresholds come from the options: every configuration starts cold again
@@ -3873,13 +3938,16 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   std::vector<rt_bvh_node> nodes(s->nodes, s->nodes + s->n_nodes);
   std::vector<rt_object> objects(s->objects, s->objects + s->n_objects);
   std::vector<float2> pmargin(s->n_prims, make_float2(-INFINITY, -INFINITY));
+  // (pvalid of a primitive outside every BVH: safe = -inf, so chain_ok's first test never applies)
+  std::vector<float4> pvalid(3 * (size_t)s->n_prims, make_float4(0.0f, 0.0f, 0.0f, -INFINITY));
   std::vector<int> tree_pairs(objects.size(), 0);  // records of each BVH object's traversal tree
   for (size_t k = 0; k < objects.size(); ++k) {
     rt_object& o = objects[k];
     o.c = -1;
     if (o.kind == RT_OBJ_MEDIUM && medium_inert(s, o)) o.c = 1;  // object_query skips it for sane rays
     if (o.kind == RT_OBJ_BVH) {
-      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes, pmargin, &tree_pairs[k], c->opt.dedup_triangles != 0);
+      const int fast = build_traversal_tree(s, o.a, o.b, prims, nodes, pmargin, pvalid, &tree_pairs[k],
+                                            c->opt.dedup_triangles != 0);
       if (fast < 0) return fail(c, RT_ERR_SCENE, "malformed reference bvh");
       o.c = fast;
     }
@@ -3932,6 +4000,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   if ((rc = upload(c, s->materials, (size_t)s->n_materials, &dm))) return rc;
   if (pmargin.size() & 1) pmargin.push_back(make_float2(-INFINITY, -INFINITY));  // whole float4s for LDS staging
   if ((rc = upload(c, pmargin.data(), pmargin.size(), &d.pmargin))) return rc;
+  if ((rc = upload(c, pvalid.data(), pvalid.size(), &d.pvalid))) return rc;
   if ((rc = upload(c, s->textures, (size_t)s->n_textures, &d.texs))) return rc;
   if ((rc = upload(c, s->perlins, (size_t)s->n_perlins, &d.perlins))) return rc;
   // Image textures in 8x8-texel tiles (row-major tiles, row-major texels inside a tile): a texel's 2-D
@@ -4167,6 +4236,13 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   const long long pkey[K] = {c->scene_gen, a->width,   a->height,    a->spp,       a->max_depth, a->fb_first,
                              a->fb_count,  a->band_rows, a->band_first, a->band_stride, a->cam_mode};
   const bool sched = items <= (64LL << 20) && (a->flags & RT_FLAG_NO_SCHEDULE) == 0;
+  if ((a->flags & RT_FLAG_FRESH) != 0) {  // as the configuration's first launch
+    std::fill(c->perm_key, c->perm_key + K, -1LL);
+    std::fill(c->pending_key, c->pending_key + K, -1LL);
+    c->split_state = -1;
+    c->n_split = 0;
+    c->order_ok = false;
+  }
   if (sched && !std::equal(pkey, pkey + K, c->perm_key) && std::equal(pkey, pkey + K, c->pending_key) &&
       items <= c->item_cap) {  // the configuration repeats: its schedule from the measured counts
     if ((rc = build_schedule(c, items, a->spp, c->pending_segs))) return rc;
@@ -4458,6 +4534,43 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   // instead of packing into the first ceil(items / block) of them.
   const unsigned blocks = (unsigned)std::max(1LL, resident);
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  // The first launch of a configuration has no measured item costs; a probe launch estimates them:
+  // sample 0 of the first fb of every owned pixel (the item's own first sample: same state, same
+  // camera draw), into the frame buffer's first fb slice, which the launch then overwrites.  An
+  // item's estimate is its pixel's probe count times spp; the launch claims items longest first by
+  // it (and records the real counts, from which the next launch builds the schedule).  Inside the
+  // timed region: the probe is part of the draw.
+  const bool probe = sched && !have_perm && c->opt.probe_schedule != 0 && !check &&
+                     (long long)a->spp * a->fb_count >= 4 && items <= c->item_cap;
+  if (probe) {
+    const long long pitems = (long long)rows * a->width;
+    if (pitems > c->probe_cap) {
+      if (c->probe_cost) HIPCHK(c, hipFree(c->probe_cost));
+      c->probe_cost = nullptr;
+      c->probe_cap = 0;
+      HIPCHK(c, hipMalloc((void**)&c->probe_cost, (size_t)pitems * sizeof(uint16_t)));
+      c->probe_cap = pitems;
+    }
+    RenderParams Q = P;
+    Q.spp = 1;
+    Q.fb_count = 1;
+    Q.total_items = (unsigned long long)pitems;
+    Q.perm = nullptr;
+    Q.n_long = 0;
+    Q.item_cost = c->probe_cost;
+    Q.row_cost = nullptr;
+    Q.split_mode = 0;
+    void* qargs[] = {&Q};
+    HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), qargs, shmem, c->stream));
+    HIPCHK(c, hipGetLastError());
+    probe_expand_kernel<<<(unsigned)std::min<long long>(4096, (items + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
+        c->probe_cost, c->item_cost, (unsigned long long)items, a->width, a->fb_count, a->spp);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemsetAsync(c->work, 0, 8 * sizeof(unsigned long long), c->stream));
+    if ((rc = build_schedule(c, items, a->spp, 0ull))) return rc;
+    P.perm = c->perm;
+    P.n_long = c->n_long;
+  }
   RT_STEP_COUNT_HOST_RESET();
   RT_STAMP_HOST_RESET();
   RT_WAVE_HOST_RESET();
@@ -4469,7 +4582,8 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-  c->last_sched = (have_perm ? RT_SCHED_PREVIOUS : 0) | (split_mode == 2 ? RT_SCHED_SPLIT_REPLAY : 0);
+  c->last_sched = (have_perm ? RT_SCHED_PREVIOUS : 0) | (split_mode == 2 ? RT_SCHED_SPLIT_REPLAY : 0) |
+                  (probe ? RT_SCHED_PROBE : 0);
   snprintf(c->last_kernel, sizeof(c->last_kernel), "%s<%d>",
            (kVariants[var].mask & F_STEP) != 0 ? "render_step_kernel" : "render_kernel", kVariants[var].mask);
   unsigned long long host_cnt[8];

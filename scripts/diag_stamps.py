@@ -1,4 +1,4 @@
-"""Diagnostic: phase shares of the render loop from a -DRT_STAMPS build (RT_HIP_LIB=<that .so>).
+"""Diagnostic: phase shares of the render loop from a -DRT_DIAG=2 build (scripts/build_ab.sh stamps raytracing_gpu_amd/csrc/rt_kernels.hip -DRT_DIAG=2) (RT_HIP_LIB=<that .so>).
 
 usage: diag_stamps.py scene W H spp nfb [nolds]
 Shares only: the stamps' own fences change the run time (cdna_hip_programming.md section 7).

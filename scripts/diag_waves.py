@@ -1,4 +1,4 @@
-"""Diagnostic: wave timeline of one render launch from a -DRT_WAVE_TIMES build (RT_HIP_LIB=<that .so>).
+"""Diagnostic: wave timeline of one render launch from a -DRT_DIAG=4 build (RT_HIP_LIB=<that .so>).
 
 usage: diag_waves.py [stride]   C2, rank 0 of `stride` ranks (4-row bands); prints when waves see the
 global work counter exhausted and when they end, relative to the first wave's start.

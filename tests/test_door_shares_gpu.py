@@ -50,16 +50,20 @@ def _upload_door(rtlib, ctx, tex):
 
 
 def _launches(rtlib, ctx, W, H, spp, nfb, cam, band, n):
-    """n launches of one configuration (the first cold); yields (frame buffer [nfb, rows, W, 3], rows,
+    """n launches of one configuration (the first cold; n may be a list of flags: True = an
+    RT_FLAG_FRESH launch, one that forgets the schedule first); yields (frame buffer [nfb, rows, W, 3], rows,
     counters, schedule bits) per launch, after checking the product kernel ran."""
     import torch
 
     args = rtlib.make_args(W, H, spp, 0, nfb, 50, cam, band_rows=band[0], band_first=band[1], band_stride=band[2])
+    fresh = rtlib.make_args(W, H, spp, 0, nfb, 50, cam, band_rows=band[0], band_first=band[1], band_stride=band[2],
+                            fresh=True)
     rows = rtlib.owned_rows(args)
-    for _ in range(n):
+    for k in range(n if isinstance(n, int) else len(n)):
+        a = args if isinstance(n, int) or not n[k] else fresh
         ctx.render_init(W, H, 1984)
         fb = torch.full((nfb * len(rows) * W * 3,), float("nan"), dtype=torch.float32, device="cuda")
-        cnt = ctx.render(args, fb.data_ptr())
+        cnt = ctx.render(a, fb.data_ptr())
         name = ctx.last_render_kernel()
         assert name.startswith("render_step_kernel<") and int(name.split("<")[1].rstrip(">")) & F_QLDS, name
         yield fb.cpu().numpy().reshape(nfb, len(rows), W, 3), rows, cnt, ctx.last_render_schedule()
@@ -80,7 +84,32 @@ def test_door_share_every_row(rtlib, gpu_ctx, oracle, n, rank):
             diff = (_bits(got[f]) != _bits(want[f][rows])).any(axis=2)
             assert not diff.any(), f"door rank {rank}/{n} launch {k} fb {f}: {int(diff.sum())} pixels differ"
         assert cnt["samples"] == nfb * len(rows) * W * spp
-    assert seen[0] == 0 and all(s & rtlib.RT_SCHED_PREVIOUS for s in seen[1:]), seen
+    assert seen[0] == rtlib.RT_SCHED_PROBE and all(s & rtlib.RT_SCHED_PREVIOUS for s in seen[1:]), seen
+    assert len(segs) == 1
+
+
+@pytest.mark.parametrize("probe", [1, 0], ids=["probe", "no_probe"])
+@pytest.mark.parametrize("cam", [REF, PIX], ids=["ref", "per_pixel"])
+def test_door_fresh_launches(rtlib, gpu_ctx, ctx_opts, oracle, cam, probe):
+    """One-shot draws (RT_FLAG_FRESH) between scheduled ones, rank 3 of 4: a fresh launch runs as the
+    configuration's first (probe launch into the first fb slice, items longest first by its estimate;
+    options.probe_schedule = 0: natural order) and the launch after it builds the schedule from the
+    fresh launch's real counts.  Every launch equals the oracle bit for bit."""
+    W, H, spp, nfb, tex = 320, 180, 4, 2, (1024, 1024)
+    want = _oracle_frames(W, H, spp, nfb, cam, tex)
+    ctx_opts(probe_schedule=probe)
+    _upload_door(rtlib, gpu_ctx, tex)
+    pattern = [True, False, False, True, False, True]
+    seen, segs = [], set()
+    for k, (got, rows, cnt, sched) in enumerate(_launches(rtlib, gpu_ctx, W, H, spp, nfb, cam, (4, 3, 4), pattern)):
+        seen.append(sched)
+        segs.add(cnt["segments"])
+        for f in range(nfb):
+            assert np.array_equal(_bits(got[f]), _bits(want[f][rows])), f"launch {k} fb {f}"
+        assert cnt["samples"] == nfb * len(rows) * W * spp
+    first = rtlib.RT_SCHED_PROBE if probe else 0
+    assert [s == first for s in seen] == pattern, seen
+    assert seen[1] & rtlib.RT_SCHED_PREVIOUS and seen[4] & rtlib.RT_SCHED_PREVIOUS, seen
     assert len(segs) == 1
 
 
