@@ -106,7 +106,7 @@ class rt_ctx_options(ctypes.Structure):
                 ("cost_shift", c_int32), ("long_pct", c_float), ("probe_schedule", c_int32)]
 
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 RT_MERGE_ON, RT_MERGE_OFF, RT_MERGE_FALLBACK_ALL = range(3)

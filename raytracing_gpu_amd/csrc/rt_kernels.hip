@@ -1752,8 +1752,8 @@ struct RenderParams {
   DScene S;
   const uint4* states;  // 2 uint4 per slot: d v0 v1 v2 | v3 v4 - -
   float* fb;
-  const int32_t* row_map;     // owned row r -> image row j (output layout order)
-  const int32_t* row_order;   // processing position q -> owned row r (costliest first)
+  const int2* row_q;          // processing position q -> {owned row r (output layout order), image
+                              // row j}: rows costliest first (one load at an item's start)
   unsigned long long* row_cost;  // per image row: segments of the finished items with i % 16 == 0
   unsigned long long* work;
   unsigned long long* counters;  // segments, node, prim, samples
@@ -1987,16 +1987,17 @@ void render_kernel(const RenderParams P) {
             ck = (int)mine;
           }
           item = P.perm ? (long long)P.perm[pos] : (long long)pos;
-          // Row-major, fb inside the row, rows in row_order: the costliest rows of the previous
+          // Row-major, fb inside the row, rows in row_q order: the costliest rows of the previous
           // launch of this configuration first (else bottom to top), so a launch does not end
           // with a long item started late (a lane runs an item's samples serially).
           const long long per_row = (long long)P.fb_count * P.W;
           const int q = (int)(item / per_row);
           const long long rem = item - (long long)q * per_row;
-          r = P.row_order[q];
+          const int2 rj = P.row_q[q];
+          r = rj.x;
           f = (int)(rem / P.W);
           i = (int)(rem - (long long)f * P.W);
-          j = P.row_map[r];
+          j = rj.y;
           const long long id = P.fb_first + f;
           const long long p = (long long)j * P.W + i;
           const long long slot = ((id + 1) * p + id + 1) % P.npix;  // render.h:101 (H3)
@@ -2392,10 +2393,11 @@ void render_step_kernel(const RenderParams P) {
             const long long per_row = (long long)P.fb_count * P.W;  // same item order as render_kernel
             const int q = (int)(item / per_row);
             const long long rem = item - (long long)q * per_row;
-            r = P.row_order[q];
+            const int2 rj = P.row_q[q];
+            r = rj.x;
             f = (int)(rem / P.W);
             i = (int)(rem - (long long)f * P.W);
-            j = P.row_map[r];
+            j = rj.y;
             const long long id = P.fb_first + f;
             const long long p = (long long)j * P.W + i;
             const long long slot = ((id + 1) * p + id + 1) % P.npix;  // render.h:101 (H3)
@@ -2619,7 +2621,7 @@ __global__ __launch_bounds__(kBlock) void merge_split_kernel(const RenderParams 
   const long long per_row = (long long)P.fb_count * P.W;
   const int q = (int)(item / per_row);
   const long long rem = item - (long long)q * per_row;
-  const int r = P.row_order[q];
+  const int r = P.row_q[q].x;
   const int f = (int)(rem / P.W);
   const int i = (int)(rem - (long long)f * P.W);
   V col = mk(0.0f, 0.0f, 0.0f);
@@ -2891,7 +2893,7 @@ struct rt_ctx {
   uint32_t* seq = nullptr;
   uint32_t* jump_tab = nullptr;  // byte tables of the subsequence jumps (init_states_kernel)
   unsigned long long* work = nullptr;  // [0] work counter, [1..4] counters
-  int32_t* row_map = nullptr;  // [rows] owned row -> image row, then [rows] processing order
+  int32_t* row_map = nullptr;  // [rows] {owned row r, image row j} in processing order (RenderParams::row_q)
   std::vector<int32_t> row_map_host;  // what row_map holds (uploaded only when it changes)
   int row_cap = 0;
   unsigned long long* row_cost = nullptr;  // device, per image row
@@ -4267,8 +4269,13 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     std::stable_sort(rm.begin() + rows, rm.end(), [&](int x, int y) { return c->host_cost[rm[x]] > c->host_cost[rm[y]]; });
   // Per-launch host work kept off the repeat path: the row tables are uploaded only when they
   // change, the row costs are cleared and read back only on their measuring launch.
-  if (rm != c->row_map_host) {
-    c->row_map_host = rm;  // kept alive for the async copy
+  std::vector<int32_t> rq(2 * (size_t)rows);
+  for (int q = 0; q < rows; ++q) {
+    rq[2 * (size_t)q] = rm[rows + q];
+    rq[2 * (size_t)q + 1] = rm[rm[rows + q]];
+  }
+  if (rq != c->row_map_host) {
+    c->row_map_host = rq;  // kept alive for the async copy
     HIPCHK(c, hipMemcpyAsync(c->row_map, c->row_map_host.data(), 2 * (size_t)rows * sizeof(int32_t),
                              hipMemcpyHostToDevice, c->stream));
   }
@@ -4281,8 +4288,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   P.S = c->scene;
   P.states = c->states;
   P.fb = fb_dev;
-  P.row_map = c->row_map;
-  P.row_order = c->row_map + rows;
+  P.row_q = (const int2*)c->row_map;
   P.row_cost = measure_rows ? c->row_cost : nullptr;  // measured once per configuration
   P.work = c->work;
   P.counters = c->work + 1;
