@@ -103,7 +103,8 @@ class rt_ctx_options(ctypes.Structure):
     _fields_ = [("world_tree", c_int32), ("quantized_tree", c_int32), ("merged_search", c_int32),
                 ("merge_order", c_int32), ("dedup_triangles", c_int32), ("shade_min", c_int32),
                 ("bins_min_items_per_lane", c_float), ("split_min_segments", c_float), ("split_order", c_int32),
-                ("cost_shift", c_int32), ("long_pct", c_float), ("probe_schedule", c_int32)]
+                ("cost_shift", c_int32), ("long_pct", c_float), ("probe_schedule", c_int32),
+                ("probe_max_items_per_lane", c_float)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

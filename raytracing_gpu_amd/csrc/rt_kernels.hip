@@ -1761,7 +1761,8 @@ struct RenderParams {
   long long npix;  // W*H of the full image
   int W, H, rows, spp, fb_first, max_depth, cam_mode, fb_count;
   int shade_min;  // render_step_kernel: lanes waiting before a wave runs its shading phase
-  int pad4;
+  int pstep;      // item grid step (1; a probe launch's grid of every pstep-th row position and pixel)
+  long long per_row;  // items per row position: fb_count * W (a probe launch: its grid's width)
   // Item schedule (see rt_render): perm maps the claimed position to the item (null: identity);
   // positions below n_long hold the longest items of the previous launch, longest first, and the
   // waves holding one run at raised priority.  item_cost (measuring launch) receives each item's
@@ -1990,13 +1991,15 @@ void render_kernel(const RenderParams P) {
           // Row-major, fb inside the row, rows in row_q order: the costliest rows of the previous
           // launch of this configuration first (else bottom to top), so a launch does not end
           // with a long item started late (a lane runs an item's samples serially).
-          const long long per_row = (long long)P.fb_count * P.W;
-          const int q = (int)(item / per_row);
-          const long long rem = item - (long long)q * per_row;
-          const int2 rj = P.row_q[q];
+          // (probe launches: items on a grid of every pstep-th row position and pixel, per_row = the
+          // grid's width; otherwise pstep = 1, per_row = fb_count * W)
+          const long long per_row = P.per_row;
+          const int qi = (int)(item / per_row);
+          const long long rem = item - (long long)qi * per_row;
+          const int2 rj = P.row_q[qi * P.pstep];
           r = rj.x;
           f = (int)(rem / P.W);
-          i = (int)(rem - (long long)f * P.W);
+          i = (int)(rem - (long long)f * P.W) * P.pstep;
           j = rj.y;
           const long long id = P.fb_first + f;
           const long long p = (long long)j * P.W + i;
@@ -2390,13 +2393,13 @@ void render_step_kernel(const RenderParams P) {
             }
             item = P.perm ? (long long)P.perm[pos] : (long long)pos;
             lng = pos < P.n_long ? 1 : 0;
-            const long long per_row = (long long)P.fb_count * P.W;  // same item order as render_kernel
-            const int q = (int)(item / per_row);
-            const long long rem = item - (long long)q * per_row;
-            const int2 rj = P.row_q[q];
+            const long long per_row = P.per_row;  // same item order as render_kernel
+            const int qi = (int)(item / per_row);
+            const long long rem = item - (long long)qi * per_row;
+            const int2 rj = P.row_q[qi * P.pstep];
             r = rj.x;
             f = (int)(rem / P.W);
-            i = (int)(rem - (long long)f * P.W);
+            i = (int)(rem - (long long)f * P.W) * P.pstep;
             j = rj.y;
             const long long id = P.fb_first + f;
             const long long p = (long long)j * P.W + i;
@@ -3364,16 +3367,43 @@ int sort_scatter(rt_ctx* c, long long n, const unsigned* base, uint32_t* out) {
   return RT_OK;
 }
 
-// Probe estimate of every item: its pixel's probe count (sample 0 of the first fb) times spp.  Items
-// are row-major with the fb inside the row (render kernels); the probe launch's items are (row, pixel).
+// Mean of the probe counts within kProbeRadius grid points (rows and pixels, clipped at the edges):
+// one sample's count is a noisy estimate of a pixel's cost, a neighbourhood's mean is a steadier one.
+// Measured (MI355X, one GPU rendering each rank's share, first launches, median of 3; probe of every
+// pixel), cold share ms at N = 4 / 8: C2 10 x 10 no probe 5.87 / 4.17, radius 0 7.02 / 5.10, 2 5.64 /
+// 4.02, 5 5.65 / 4.12; C4 no probe 32.86 / 26.70, radius 0 28.14 / 27.87, 2 27.49 / 27.08, 5 25.58 /
+// 25.12 (profiles/r05/probe/psc_*.txt).
+constexpr int kProbeRadius = 5;
+__global__ __launch_bounds__(kBlock) void probe_smooth_kernel(const uint16_t* __restrict__ raw,
+                                                              uint16_t* __restrict__ out, int prow, int pw) {
+  const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= (long long)prow * pw) return;
+  const int q = (int)(k / pw), i = (int)(k - (long long)q * pw);
+  unsigned sum = 0, n = 0;
+  for (int dq = -kProbeRadius; dq <= kProbeRadius; ++dq) {
+    const int qq = q + dq;
+    if (qq < 0 || qq >= prow) continue;
+    for (int di = -kProbeRadius; di <= kProbeRadius; ++di) {
+      const int ii = i + di;
+      if (ii < 0 || ii >= pw) continue;
+      sum += raw[(long long)qq * pw + ii];
+      ++n;
+    }
+  }
+  out[k] = (uint16_t)((sum + n / 2) / n);
+}
+
+// Probe estimate of every item: the (smoothed) probe count of its grid point (sample 0 of the first fb at row
+// position ps * (q / ps), pixel ps * (i / ps)) times spp.  Items are row-major with the fb inside the
+// row (render kernels); the probe launch's items are the grid's (row position, pixel) points.
 __global__ __launch_bounds__(kBlock) void probe_expand_kernel(const uint16_t* __restrict__ probe,
                                                               uint16_t* __restrict__ cost, unsigned long long items,
-                                                              int W, int fbc, int spp) {
+                                                              int W, int fbc, int spp, int ps, int pw) {
   const unsigned long long per_row = (unsigned long long)fbc * (unsigned)W;
   for (unsigned long long k = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; k < items;
        k += (unsigned long long)gridDim.x * blockDim.x) {
     const unsigned long long q = k / per_row, i = (k - q * per_row) % (unsigned)W;
-    const unsigned v = (unsigned)probe[q * (unsigned)W + i] * (unsigned)spp;
+    const unsigned v = (unsigned)probe[(q / (unsigned)ps) * (unsigned)pw + i / (unsigned)ps] * (unsigned)spp;
     cost[k] = (uint16_t)(v < 65535u ? v : 65535u);
   }
 }
@@ -3589,6 +3619,7 @@ void rt_ctx_options_default(rt_ctx_options* o) {
   o->cost_shift = -1;
   o->long_pct = 2.0f;
   o->probe_schedule = 1;
+  o->probe_max_items_per_lane = 33.0f;
 }
 
 int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
@@ -3597,7 +3628,7 @@ int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
       o->merge_order < RT_ORDER_DISTANCE || o->merge_order > RT_ORDER_REVERSED || o->shade_min < 0 ||
       o->shade_min > 64 || !(o->bins_min_items_per_lane >= 0.0f) || !(o->split_min_segments >= 0.0f) ||
       o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f) || o->probe_schedule < 0 ||
-      o->probe_schedule > 1)
+      o->probe_schedule > 64 || !(o->probe_max_items_per_lane >= 0.0f))
     return fail(c, RT_ERR_ARG, "bad context options");
   c->opt = *o;
   // the schedule and split thresholds come from the options: every configuration starts cold again
@@ -4297,6 +4328,8 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   P.W = a->width;
   P.H = a->height;
   P.rows = rows;
+  P.pstep = 1;
+  P.per_row = (long long)a->fb_count * a->width;
   P.spp = a->spp;
   P.fb_first = a->fb_first;
   P.fb_count = a->fb_count;
@@ -4539,28 +4572,34 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   // rank of a multi-GPU run): waves take items dynamically, so the items spread over all CUs
   // instead of packing into the first ceil(items / block) of them.
   const unsigned blocks = (unsigned)std::max(1LL, resident);
-  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   // The first launch of a configuration has no measured item costs; a probe launch estimates them:
-  // sample 0 of the first fb of every owned pixel (the item's own first sample: same state, same
-  // camera draw), into the frame buffer's first fb slice, which the launch then overwrites.  An
-  // item's estimate is its pixel's probe count times spp; the launch claims items longest first by
-  // it (and records the real counts, from which the next launch builds the schedule).  Inside the
-  // timed region: the probe is part of the draw.
-  const bool probe = sched && !have_perm && c->opt.probe_schedule != 0 && !check &&
-                     (long long)a->spp * a->fb_count >= 4 && items <= c->item_cap;
+  // sample 0 of the first fb (the item's own first sample: same state, same camera draw) at every
+  // ps-th owned row position and pixel, into the frame buffer's first fb slice, which the launch then
+  // overwrites.  An item's estimate is the mean count of the grid points within kProbeRadius of its
+  // own (rows and pixels) times spp; the launch claims items longest first by it (and records the
+  // real counts, from which the next launch builds the schedule).  Inside the timed region: the
+  // probe is part of the draw.  Only for a small share (a rank of a multi-GPU image), whose launch
+  // ends with its longest items.
+  const int ps = c->opt.probe_schedule;  // probe grid step (0: no probe)
+  const bool probe = sched && !have_perm && ps > 0 && !check && (long long)a->spp * a->fb_count >= 4 &&
+                     items <= c->item_cap && (double)items < (double)c->opt.probe_max_items_per_lane * lanes;
+  const int prow = (rows + ps - 1) / std::max(1, ps), pw = (a->width + ps - 1) / std::max(1, ps);
+  const long long pitems = (long long)prow * pw;
+  if (probe && pitems > c->probe_cap) {  // raw counts, then the smoothed grid
+    if (c->probe_cost) HIPCHK(c, hipFree(c->probe_cost));
+    c->probe_cost = nullptr;
+    c->probe_cap = 0;
+    HIPCHK(c, hipMalloc((void**)&c->probe_cost, 2 * (size_t)pitems * sizeof(uint16_t)));
+    c->probe_cap = pitems;
+  }
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   if (probe) {
-    const long long pitems = (long long)rows * a->width;
-    if (pitems > c->probe_cap) {
-      if (c->probe_cost) HIPCHK(c, hipFree(c->probe_cost));
-      c->probe_cost = nullptr;
-      c->probe_cap = 0;
-      HIPCHK(c, hipMalloc((void**)&c->probe_cost, (size_t)pitems * sizeof(uint16_t)));
-      c->probe_cap = pitems;
-    }
     RenderParams Q = P;
     Q.spp = 1;
     Q.fb_count = 1;
     Q.total_items = (unsigned long long)pitems;
+    Q.pstep = ps;
+    Q.per_row = pw;
     Q.perm = nullptr;
     Q.n_long = 0;
     Q.item_cost = c->probe_cost;
@@ -4569,8 +4608,11 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     void* qargs[] = {&Q};
     HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), qargs, shmem, c->stream));
     HIPCHK(c, hipGetLastError());
+    probe_smooth_kernel<<<(unsigned)((pitems + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
+        c->probe_cost, c->probe_cost + pitems, prow, pw);
+    HIPCHK(c, hipGetLastError());
     probe_expand_kernel<<<(unsigned)std::min<long long>(4096, (items + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
-        c->probe_cost, c->item_cost, (unsigned long long)items, a->width, a->fb_count, a->spp);
+        c->probe_cost + pitems, c->item_cost, (unsigned long long)items, a->width, a->fb_count, a->spp, ps, pw);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemsetAsync(c->work, 0, 8 * sizeof(unsigned long long), c->stream));
     if ((rc = build_schedule(c, items, a->spp, 0ull))) return rc;

@@ -2,8 +2,9 @@
 
 For N in 1, 2, 4, 8 and every rank r < N, times rank r's step pieces as bench.py runs them
 (render_init, the render of its 4-row bands, resolve) with HIP events; the N-GPU step is bounded
-below by max over ranks.  "cold" is a rank's first launch of its configuration (no longest-first
-item schedule yet: the reference's single draw()), "warm" the best of launches 3 and 4 (launch 2 records the split items' sample-start states).  The gather
+below by max over ranks.  "cold" is a rank's first launch of its configuration (no item schedule yet: the reference's single
+draw(); the median of three RT_FLAG_FRESH launches), "warm" the best of the 2nd and 3rd launch after
+them (the 1st records the split items' sample-start states).  The gather
 is modelled from its bytes (N x the largest share's 8-bit rows) at XGMI_GBS (default 64 GB/s,
 a conservative all-gather rate for a few MB over xGMI) plus 30 us of collective latency.
 
@@ -53,6 +54,10 @@ def host_timed(fn):  # render_init runs on the context's own stream: time it to 
     return (time.perf_counter() - t0) * 1e3
 
 
+# module load + first allocations on a tiny image (a different configuration), as bench.py does
+ctx.render_init(64, 36, 1984)
+_tfb = torch.empty(64 * 36 * 3, dtype=torch.float32, device="cuda")
+ctx.render(rt.make_args(64, 36, 1, 0, 1, 50, 0), _tfb.data_ptr())
 t_init = min(host_timed(lambda: ctx.render_init(W, H, 1984)) for _ in range(5))
 xgmi = float(os.environ.get("XGMI_GBS", "64"))
 base = None
@@ -67,18 +72,27 @@ for n in (1, 2, 4, 8):
         rows = rt.owned_rows(args)
         fb = torch.empty(nfb * len(rows) * W * 3, dtype=torch.float32, device="cuda")
         img = torch.empty(len(rows) * W * 3, dtype=torch.uint8, device="cuda")
-        ms = []
-        for _ in range(4):  # launch 1 measures the item costs, 2 records split states, 3+ are warm
+        fargs = rt.make_args(W, H, spp, 0, nfb, 50, 0, band_rows=4, band_first=r, band_stride=n,
+                             bins=os.environ.get("DIAG_BINS", "1") != "0", fresh=True)
+        cold_ms, bits = [], []
+        for _ in range(3):  # first launches of the configuration (RT_FLAG_FRESH): the median
+            ctx.render(fargs, fb.data_ptr())
+            cold_ms.append(ctx.last_render_ms())
+            bits.append(ctx.last_render_schedule())
+        ms = [sorted(cold_ms)[1]]
+        for _ in range(3):  # the 1st builds the schedule and records split states, 2nd+ are warm
             c = ctx.render(args, fb.data_ptr())
             ms.append(ctx.last_render_ms())
+            bits.append(ctx.last_render_schedule())
         t_res = min(timed(lambda: ctx.resolve(args, fb.data_ptr(), img.data_ptr())) for _ in range(3))
         worst = max(worst, min(ms[2:]) + t_res)
         worst_cold = max(worst_cold, ms[0] + t_res)
         share_rows = max(share_rows, len(rows))
         segs += c["segments"]
         if os.environ.get("VERBOSE"):
-            print(f"   N={n} rank {r}: warm {min(ms[2:]):.2f} ms, cold {ms[0]:.2f} ms, 2nd {ms[1]:.2f} ms, "
-                  f"{c['segments']} segments, {c['segments'] / min(ms[2:]) / 1e3:.0f} Mrays/s", flush=True)
+            print(f"   N={n} rank {r}: warm {min(ms[2:]):.2f} ms, cold {ms[0]:.2f} ms {[round(x, 2) for x in cold_ms]}, "
+                  f"1st scheduled {ms[1]:.2f} ms, "
+                  f"{c['segments']} segments, {c['segments'] / min(ms[2:]) / 1e3:.0f} Mrays/s, schedule bits {bits}", flush=True)
     gbytes = n * share_rows * W * 3 if n > 1 else 0
     t_gather = (gbytes / (xgmi * 1e6) + 0.03) if n > 1 else 0.0
     step = worst + t_init + t_gather

@@ -88,13 +88,14 @@ def test_door_share_every_row(rtlib, gpu_ctx, oracle, n, rank):
     assert len(segs) == 1
 
 
-@pytest.mark.parametrize("probe", [1, 0], ids=["probe", "no_probe"])
+@pytest.mark.parametrize("probe", [4, 1, 0], ids=["probe_grid4", "probe_every_pixel", "no_probe"])
 @pytest.mark.parametrize("cam", [REF, PIX], ids=["ref", "per_pixel"])
 def test_door_fresh_launches(rtlib, gpu_ctx, ctx_opts, oracle, cam, probe):
     """One-shot draws (RT_FLAG_FRESH) between scheduled ones, rank 3 of 4: a fresh launch runs as the
-    configuration's first (probe launch into the first fb slice, items longest first by its estimate;
-    options.probe_schedule = 0: natural order) and the launch after it builds the schedule from the
-    fresh launch's real counts.  Every launch equals the oracle bit for bit."""
+    configuration's first (probe launch on every probe-th row and pixel into the first fb slice,
+    items longest first by its estimate; options.probe_schedule = 0: natural order) and the launch
+    after it builds the schedule from the fresh launch's real counts.  Every launch equals the oracle
+    bit for bit."""
     W, H, spp, nfb, tex = 320, 180, 4, 2, (1024, 1024)
     want = _oracle_frames(W, H, spp, nfb, cam, tex)
     ctx_opts(probe_schedule=probe)
