@@ -242,7 +242,7 @@ typedef struct rt_ctx_options {
                                 group stands for it (default 1)                                     */
   /* per launch (rt_render) */
   int32_t shade_min;         /* stepwise kernel: lanes waiting before a wave shades; 0 = the
-                                variant's measured value (60, 56 for triangle meshes)               */
+                                variant's measured value (60, 48 for triangle meshes)               */
   float bins_min_items_per_lane; /* camera-ray tile lists from this many items per resident lane
                                 (default 6; 0 = always)                                             */
   float split_min_segments;  /* > 0: split the samples of items of at least this many segments;

@@ -1806,8 +1806,17 @@ constexpr int kTileCap = 32;   // entries per tile list (a fuller tile traverses
 // render_kernel refills a wave once this many lanes are idle (same box, Mrays/s at 16 / 8 / 4 / 2 / 1:
 // C3 18 854 / 20 165 / 20 590 / 20 571 / 20 645, C5 3 749 / 3 829 / 3 828 / 3 813 / 3 745)
 constexpr int kRefill = 4;
+// render_step_kernel refills a wave once this many lanes are idle (or none is busy): at every idle
+// lane for the sphere variants (C2 at 4 / 8: 14 930 -> 14 796 / 14 498 Mrays/s), at 4 for the mesh
+// variants, whose refill (state, row and tile-list loads from global memory behind the traversal's
+// own global loads) stalls the whole wave (C4 at 1 / 2 / 3 / 4 / 6: 18 144 / 18 513 / 18 697 /
+// 18 741 / 18 659 Mrays/s; profiles/r05/refill_ab.txt)
+template <int F>
+constexpr int step_refill() { return (F & F_TRI) != 0 ? 4 : 1; }
 constexpr int kShadeMin = 60;  // render_step_kernel: default shading-phase threshold
-constexpr int kShadeMinMesh = 56;  // ... for triangle-mesh variants (48 before the triangle dedupe)
+constexpr int kShadeMinMesh = 48;  // ... for triangle-mesh variants (round 5, with step_refill 4: C4 at
+                                   // 36 / 40 / 44 / 48 / 52 / 56 / 60: 18 845 / 18 971 / 19 048 / 19 079 /
+                                   // 19 021 / 18 750 / 17 986 Mrays/s; profiles/r05/shade_ab.txt)
 constexpr int kShadePasses = 2;    // render_step_kernel: shading passes per phase (1: C2 17.2 -> 20.4 ms, 3: +0.7 %)
 constexpr unsigned kChunk = 64;  // items a wave claims per work-counter atomic
 static_assert(kChunk >= 64, "claim_items: one claim must cover a refill of every lane of a wave");
@@ -2368,7 +2377,7 @@ void render_step_kernel(const RenderParams P) {
       // ---- refill lanes without an item from the wave's chunk of the work counter (one atomic
       // per kChunk items: a single counter serialises its atomics in L2)
       const unsigned long long idle = __ballot(item < 0 && !done);
-      if (idle != 0) {
+      if (idle != 0 && (__popcll(idle) >= step_refill<F>() || __ballot(item >= 0) == 0)) {
         const unsigned long long mine = claim_items(P.work, idle, chunk_base, chunk_left);
         if (item < 0 && !done) {
           if (mine >= P.total_items) {
