@@ -4588,10 +4588,15 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   // own (rows and pixels) times spp; the launch claims items longest first by it (and records the
   // real counts, from which the next launch builds the schedule).  Inside the timed region: the
   // probe is part of the draw.  Only for a small share (a rank of a multi-GPU image), whose launch
-  // ends with its longest items.
+  // ends with its longest items, of a scene with BVHs: list worlds of rects and media (C3) lost at
+  // every share size (cold ms, N = 1 / 2 / 4 / 8, without / with: 14.73 / 8.10 / 4.93 / 3.23 vs 15.64 /
+  // 8.94 / 5.70 / 4.04), their costs are short and spatially random and the natural order's coherence
+  // wins; C2 1 x 100 at N = 1 (3.7 items per lane) 29.3 -> 26.1 ms, C5 N = 4 23.72 -> 22.36 ms
+  // (profiles/r05/probe/).
   const int ps = c->opt.probe_schedule;  // probe grid step (0: no probe)
   const bool probe = sched && !have_perm && ps > 0 && !check && (long long)a->spp * a->fb_count >= 4 &&
-                     items <= c->item_cap && (double)items < (double)c->opt.probe_max_items_per_lane * lanes;
+                     (vmask & (F_STEP | F_BVH)) != 0 && items <= c->item_cap &&
+                     (double)items < (double)c->opt.probe_max_items_per_lane * lanes;
   const int prow = (rows + ps - 1) / std::max(1, ps), pw = (a->width + ps - 1) / std::max(1, ps);
   const long long pitems = (long long)prow * pw;
   if (probe && pitems > c->probe_cap) {  // raw counts, then the smoothed grid
