@@ -252,12 +252,14 @@ typedef struct rt_ctx_options {
   int32_t cost_shift;        /* item-schedule cost buckets of 2^cost_shift segments; -1 = automatic */
   float long_pct;            /* share of the longest items whose waves run at raised priority
                                 (default 2)                                                         */
-  int32_t probe_schedule;    /* k > 0: the first launch of a configuration of >= 4 samples per
-                                pixel and fewer than probe_max_items_per_lane items per resident
-                                lane (a small share) claims its items longest first by a probe
-                                launch's estimate (sample 0 of the first fb at every k-th row and
-                                pixel, output discarded); 0: natural order (default 1, at most 64)  */
-  float probe_max_items_per_lane; /* (default 33; C4's 4-GPU share has 31.7)                        */
+  int32_t probe_schedule;    /* k > 0: the first launch of a configuration (>= 4 samples per pixel,
+                                a scene with BVHs) claims its items longest first by a probe
+                                launch's estimate: sample 0 of the first fb at every k-th row and
+                                pixel (output discarded), smoothed over neighbouring grid points;
+                                -1 (default): the smallest k with k*k*spp*fb_count >= 200; 0: natural
+                                order; at most 64                                                   */
+  float probe_max_items_per_lane; /* > 0: probe only launches with fewer items per resident lane (a
+                                multi-GPU share); 0 (default): any launch                           */
 } rt_ctx_options;
 void rt_ctx_options_default(rt_ctx_options* opts);
 int rt_ctx_set_options(rt_ctx* ctx, const rt_ctx_options* opts);

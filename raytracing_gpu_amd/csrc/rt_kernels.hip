@@ -3627,8 +3627,8 @@ void rt_ctx_options_default(rt_ctx_options* o) {
   o->split_order = 1;
   o->cost_shift = -1;
   o->long_pct = 2.0f;
-  o->probe_schedule = 1;
-  o->probe_max_items_per_lane = 33.0f;
+  o->probe_schedule = -1;
+  o->probe_max_items_per_lane = 0.0f;
 }
 
 int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
@@ -3636,7 +3636,7 @@ int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
   if (o->merged_search < RT_MERGE_ON || o->merged_search > RT_MERGE_FALLBACK_ALL ||
       o->merge_order < RT_ORDER_DISTANCE || o->merge_order > RT_ORDER_REVERSED || o->shade_min < 0 ||
       o->shade_min > 64 || !(o->bins_min_items_per_lane >= 0.0f) || !(o->split_min_segments >= 0.0f) ||
-      o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f) || o->probe_schedule < 0 ||
+      o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f) || o->probe_schedule < -1 ||
       o->probe_schedule > 64 || !(o->probe_max_items_per_lane >= 0.0f))
     return fail(c, RT_ERR_ARG, "bad context options");
   c->opt = *o;
@@ -4587,16 +4587,21 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   // overwrites.  An item's estimate is the mean count of the grid points within kProbeRadius of its
   // own (rows and pixels) times spp; the launch claims items longest first by it (and records the
   // real counts, from which the next launch builds the schedule).  Inside the timed region: the
-  // probe is part of the draw.  Only for a small share (a rank of a multi-GPU image), whose launch
-  // ends with its longest items, of a scene with BVHs: list worlds of rects and media (C3) lost at
-  // every share size (cold ms, N = 1 / 2 / 4 / 8, without / with: 14.73 / 8.10 / 4.93 / 3.23 vs 15.64 /
-  // 8.94 / 5.70 / 4.04), their costs are short and spatially random and the natural order's coherence
-  // wins; C2 1 x 100 at N = 1 (3.7 items per lane) 29.3 -> 26.1 ms, C5 N = 4 23.72 -> 22.36 ms
-  // (profiles/r05/probe/).
-  const int ps = c->opt.probe_schedule;  // probe grid step (0: no probe)
+  // probe is part of the draw.  Grid step (options.probe_schedule < 0, the default): the smallest
+  // with step^2 * spp * fb_count >= 200, a probe of at most ~0.5 % of the draw's samples.  Measured
+  // (MI355X, cold first launches, no probe -> probe): whole frames C4 77.3 -> 67.0 ms (step 1; 4:
+  // 69.6), C5 67.8 -> 64.0 (step 4; 2: 65.1, 8: 64.8), C2 17.02 -> 16.96 (step 4; 1: 17.28); not for
+  // scenes without BVHs: C3's list of rects and media lost at every share size (N = 1 / 2 / 4 / 8
+  // 14.73 / 8.10 / 4.93 / 3.23 -> 15.64 / 8.94 / 5.70 / 4.04 ms), its costs short and spatially
+  // random, the natural order's coherence better (profiles/r05/probe/).
+  int ps = c->opt.probe_schedule;  // probe grid step (0: no probe)
+  if (ps < 0)
+    for (ps = 1; ps < 64 && (long long)ps * ps * a->spp * a->fb_count < 200; ++ps) {
+    }
   const bool probe = sched && !have_perm && ps > 0 && !check && (long long)a->spp * a->fb_count >= 4 &&
                      (vmask & (F_STEP | F_BVH)) != 0 && items <= c->item_cap &&
-                     (double)items < (double)c->opt.probe_max_items_per_lane * lanes;
+                     (c->opt.probe_max_items_per_lane <= 0.0f ||
+                      (double)items < (double)c->opt.probe_max_items_per_lane * lanes);
   const int prow = (rows + ps - 1) / std::max(1, ps), pw = (a->width + ps - 1) / std::max(1, ps);
   const long long pitems = (long long)prow * pw;
   if (probe && pitems > c->probe_cap) {  // raw counts, then the smoothed grid
