@@ -4277,7 +4277,9 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   constexpr int K = rt_ctx::kKey;
   const long long pkey[K] = {c->scene_gen, a->width,   a->height,    a->spp,       a->max_depth, a->fb_first,
                              a->fb_count,  a->band_rows, a->band_first, a->band_stride, a->cam_mode};
-  const bool sched = items <= (64LL << 20) && (a->flags & RT_FLAG_NO_SCHEDULE) == 0;
+  // (up to 2^31 items: 6 bytes of cost and position per item, C5's configured 100 fb x 100 spp draw
+  // has 829 M; perm holds 32-bit positions)
+  const bool sched = items <= (1LL << 31) && (a->flags & RT_FLAG_NO_SCHEDULE) == 0;
   if ((a->flags & RT_FLAG_FRESH) != 0) {  // as the configuration's first launch
     std::fill(c->perm_key, c->perm_key + K, -1LL);
     std::fill(c->pending_key, c->pending_key + K, -1LL);
