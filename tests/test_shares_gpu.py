@@ -36,12 +36,12 @@ def _assets(scene, tex_shape):
     return dict(images=[img], meshes=[m]), dict(images=[img], meshes=[(m.tris, True, 0)])
 
 
-def _share(rtlib, ctx, W, H, spp, nfb, band, launches, kernel_prefix):
+def _share(rtlib, ctx, W, H, spp, nfb, band, launches, kernel_prefix, cam=REF):
     """Render one rank's share `launches` times (cold, then scheduled); returns the last frame buffer
     as [nfb, owned rows, W, 3], the owned rows, and every launch's counters and schedule bits."""
     import torch
 
-    args = rtlib.make_args(W, H, spp, 0, nfb, 50, REF, band_rows=band[0], band_first=band[1], band_stride=band[2])
+    args = rtlib.make_args(W, H, spp, 0, nfb, 50, cam, band_rows=band[0], band_first=band[1], band_stride=band[2])
     rows = rtlib.owned_rows(args)
     got, log = None, []
     for _ in range(launches):
@@ -279,18 +279,19 @@ def test_merged_list_search_bit_exact(rtlib, gpu_ctx, oracle, ctx_opts, scene, m
                 assert cnt["segments"] == sum(int(w[1]["segments"]) for w in want)
 
 
-def test_final_share_probe_launch(rtlib, gpu_ctx, oracle):
+@pytest.mark.parametrize("cam", [REF, 1], ids=["ref", "per_pixel"])
+def test_final_share_probe_launch(rtlib, gpu_ctx, oracle, cam):
     """C5's scene as rank 1 of 4 at 320x180, 2 fb x 2 spp: the first launch of the share is
     probe-scheduled on render_kernel's merged-search variant (probe launch into the first fb slice,
     items longest first by its estimate), the next one scheduled by its real counts; both equal the
-    oracle bit for bit on every owned row."""
+    oracle bit for bit on every owned row, in both camera modes."""
     pa, oa = _assets("final", (341, 152))
     W, H, spp, nfb = 320, 180, 2, 2
     gpu_ctx.upload(rtlib.Scene.builtin("final", **pa))
-    got, rows, log = _share(rtlib, gpu_ctx, W, H, spp, nfb, (4, 1, 4), 2, "render_kernel<")
+    got, rows, log = _share(rtlib, gpu_ctx, W, H, spp, nfb, (4, 1, 4), 2, "render_kernel<", cam=cam)
     assert log[0][1] == rtlib.RT_SCHED_PROBE and log[1][1] & rtlib.RT_SCHED_PREVIOUS, log
     ref = oracle.RefScene("final", **oa)
     for f in range(nfb):
-        want = ref.render(W, H, spp, f, 50, REF)[0].reshape(H, W, 3)[rows]
+        want = ref.render(W, H, spp, f, 50, cam)[0].reshape(H, W, 3)[rows]
         diff = (_bits(got[f]) != _bits(want)).any(axis=2)
         assert not diff.any(), f"final share fb {f}: {int(diff.sum())} pixels differ"
