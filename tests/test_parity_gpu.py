@@ -655,3 +655,23 @@ def test_c2_primary_split_culled_equals_exact(rtlib, gpu_ctx):
         assert cf["segments"] == ce["segments"], f"launch {launch}"
         assert np.array_equal(_bits(fb.cpu().numpy().reshape(ex.shape)), _bits(ex)), f"launch {launch}"
 
+
+
+@pytest.mark.parametrize("grid", [3, 7])
+@pytest.mark.parametrize("band", [None, (3, 1, 2)], ids=["full", "share"])
+@pytest.mark.parametrize("cam", [REF, PIX], ids=["ref", "per_pixel"])
+def test_probe_grid_edges(rtlib, gpu_ctx, oracle, ctx_opts, grid, band, cam):
+    """Probe-scheduled first launches on grids that do not divide the image (101x57, every 3rd /
+    7th row position and pixel), fb ids 2..3 of a call, full frame and a 3-row-band share: the probe
+    writes into the first fb slice of the call, which the launch overwrites; every pixel equals the
+    oracle and the launch reports RT_SCHED_PROBE."""
+    ctx_opts(probe_schedule=grid)
+    W, H, spp, fb_first, fb_count = 101, 57, 2, 2, 2
+    gpu, rows, cnt, _, _ = _gpu_render(rtlib, gpu_ctx, "big1", W, H, spp, fb_first, fb_count, cam, band=band)
+    assert gpu_ctx.last_render_schedule() == rtlib.RT_SCHED_PROBE
+    ref = oracle.RefScene("big1")
+    for f in range(fb_count):
+        want = ref.render(W, H, spp, fb_first + f, 50, cam)[0].reshape(H, W, 3)[rows]
+        diff = (_bits(gpu[f]) != _bits(want)).any(axis=2)
+        assert not diff.any(), f"grid {grid} fb {fb_first + f}: {int(diff.sum())} pixels differ"
+    assert cnt["samples"] == len(rows) * W * spp * fb_count
