@@ -2557,13 +2557,16 @@ void render_step_kernel(const RenderParams P) {
   }
 }
 
-// curand_init(seed, slot, 0) for every slot < n (render.h:84-92).  Each lane owns kInitChunk
+// curand_init(seed, slot, 0) for every slot < n (render.h:84-92).  Each lane owns `chunk`
 // consecutive slots: one seed scramble + subsequence jump A^(first * 2^67) applied digit by digit
 // in base 4 (as skipahead_sequence: digit d at position i applies (A^(4^i * 2^67))^d), then one
 // mat-vec with A^(2^67) per following slot (state(s+1) = A^(2^67) state(s)).  Every mat-vec on
 // GF(2)^160 goes through byte tables (rt_ctx::jump_tab, built once per context): the image of the
-// state is the XOR of 20 table rows, one per state byte, instead of 160 masked row XORs.
-constexpr int kInitChunk = 16;
+// state is the XOR of 20 table rows, one per state byte, instead of 160 masked row XORs.  The
+// slot-step table (the one every following slot applies) is staged in LDS, one workgroup per CU:
+// with every table read from L2 the kernel moved ~1 GB of table rows per C2 init (105 us).
+constexpr int kInitBlock = 512;
+constexpr int kStepRows = 20 * 256;           // rows of a byte table
 constexpr int kTabRow = 8;                    // words per table row (5 used, 32-byte aligned)
 constexpr int kTabMat = 20 * 256 * kTabRow;   // words per matrix table
 __device__ __forceinline__ void tab_apply(const uint32_t* __restrict__ t, uint32_t v[5]) {
@@ -2581,10 +2584,35 @@ __device__ __forceinline__ void tab_apply(const uint32_t* __restrict__ t, uint32
   }
   v[0] = r0; v[1] = r1; v[2] = r2; v[3] = r3; v[4] = r4;
 }
+// The slot-step table in LDS as five planes (word k of row r at [k * kStepRows + r]).
+__device__ __forceinline__ void tab_apply_lds(const uint32_t* t, uint32_t v[5]) {
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
+  #pragma unroll
+  for (int b = 0; b < 20; ++b) {
+    const int row = b * 256 + (int)((v[b >> 2] >> (8 * (b & 3))) & 0xffu);
+    r0 ^= t[row];
+    r1 ^= t[kStepRows + row];
+    r2 ^= t[2 * kStepRows + row];
+    r3 ^= t[3 * kStepRows + row];
+    r4 ^= t[4 * kStepRows + row];
+  }
+  v[0] = r0; v[1] = r1; v[2] = r2; v[3] = r3; v[4] = r4;
+}
 // jump_tab: table (d - 1) * 32 + i = (A^(4^i * 2^67))^d, d = 1..3; table 0 is the slot step.
-__global__ __launch_bounds__(kBlock) void init_states_kernel(uint4* states, long long n, uint64_t seed,
-                                                            const uint32_t* __restrict__ jump_tab, int digits) {
-  const long long first = ((long long)blockIdx.x * kBlock + threadIdx.x) * kInitChunk;
+__global__ __launch_bounds__(kInitBlock) void init_states_kernel(uint4* states, long long n, uint64_t seed,
+                                                                const uint32_t* __restrict__ jump_tab, int digits,
+                                                                long long chunk) {
+  extern __shared__ uint32_t step_lds[];  // 5 * kStepRows words
+  for (int r = threadIdx.x; r < kStepRows; r += kInitBlock) {
+    const uint4 x = *(const uint4*)(jump_tab + (size_t)r * kTabRow);
+    step_lds[r] = x.x;
+    step_lds[kStepRows + r] = x.y;
+    step_lds[2 * kStepRows + r] = x.z;
+    step_lds[3 * kStepRows + r] = x.w;
+    step_lds[4 * kStepRows + r] = jump_tab[(size_t)r * kTabRow + 4];
+  }
+  __syncthreads();
+  const long long first = ((long long)blockIdx.x * kInitBlock + threadIdx.x) * chunk;
   if (first >= n) return;
   rtx::State st = rtx::seed_state(seed);
   unsigned long long x = (unsigned long long)first;
@@ -2593,8 +2621,8 @@ __global__ __launch_bounds__(kBlock) void init_states_kernel(uint4* states, long
     x >>= 2;
     if (dig != 0) tab_apply(jump_tab + (size_t)((dig - 1) * 32 + d) * kTabMat, st.v);
   }
-  for (int c = 0; c < kInitChunk && first + c < n; ++c) {
-    if (c > 0) tab_apply(jump_tab, st.v);
+  for (long long c = 0; c < chunk && first + c < n; ++c) {
+    if (c > 0) tab_apply_lds(step_lds, st.v);
     const long long slot = first + c;
     states[2 * slot] = make_uint4(st.d, st.v[0], st.v[1], st.v[2]);
     states[2 * slot + 1] = make_uint4(st.v[3], st.v[4], 0u, 0u);
@@ -4192,10 +4220,11 @@ int rt_render_init(rt_ctx* c, int32_t width, int32_t height, uint64_t seed) {
   }
   int digits = 0;
   for (unsigned long long x = (unsigned long long)(n - 1); x; x >>= 2) ++digits;
-  const long long lanes = (n + kInitChunk - 1) / kInitChunk;
-  const long long blocks = (lanes + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(init_states_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, c->stream, c->states, n, seed,
-                     (const uint32_t*)c->jump_tab, digits);
+  // one workgroup per CU (its LDS holds the 100 KB slot-step table), every lane a run of slots
+  const long long blocks = std::max(1LL, std::min<long long>(c->cus, (n + kInitBlock - 1) / kInitBlock));
+  const long long chunk = (n + blocks * kInitBlock - 1) / (blocks * kInitBlock);
+  hipLaunchKernelGGL(init_states_kernel, dim3((unsigned)blocks), dim3(kInitBlock), 5 * kStepRows * sizeof(uint32_t),
+                     c->stream, c->states, n, seed, (const uint32_t*)c->jump_tab, digits, chunk);
   HIPCHK(c, hipGetLastError());
   // no host wait: every reader of the states (rt_render's kernels, rt_read_states) is ordered
   // after this launch on the context's stream
