@@ -8,6 +8,13 @@ reference camera-RNG mode.  One step = one draw(): render_init + all 10 fb rende
 quantise/average (resolve) [+ the RCCL gather of the 8-bit rows to rank 0 when N > 1].
 A ray segment = one top-level world query (render.h:63), counted on the device.
 
+Every timed step is a ONE-SHOT draw (RT_FLAG_FRESH): the context forgets whatever it learned from
+earlier draws of the same configuration, so each step runs as the reference's single draw() does --
+the probe launch, the item schedule from its estimate, the render.  `value` and `ms_per_step` are
+those draws.  The steady state of repeating one configuration (items claimed by the previous draw's
+measured costs, split samples started from RNG states an earlier draw recorded) is reported beside
+it as `warm_value` / `warm_ms_per_step`, never as `value`.
+
 N > 1 (one process per GPU, torch.distributed over RCCL): rows are dealt in 4-row bands
 round-robin over ranks; each rank renders and resolves its rows for every fb; one all-gather of
 the 8-bit rows assembles the image.  Strong scaling (the image is fixed).
@@ -93,12 +100,14 @@ def parse():
     ap.add_argument("--no-lds", action="store_true", help="keep the scene in global memory")
     ap.add_argument("--no-step", action="store_true", help="segment-per-trip kernel even when the world is one BVH")
     ap.add_argument("--no-bins", action="store_true", help="camera rays traverse the BVH (no per-tile candidate lists)")
-    ap.add_argument("--no-schedule", action="store_true", help="every draw cold: nothing reused from an earlier launch")
+    ap.add_argument("--no-schedule", action="store_true", help="natural item order (no probe, no item schedule)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the untimed node/prim counting pass")
     ap.add_argument("--png", default="", help="write the assembled image (rank 0)")
-    ap.add_argument("--cold-steps", type=int, default=3, help="draws timed with nothing reused (cold_ms_per_step)")
+    ap.add_argument("--warm-steps", type=int, default=5,
+                    help="repeat draws timed after two priming draws (warm_*: the configuration's schedule and "
+                         "split-sample states reused; 0 = skip)")
     ap.add_argument("--gather", default="rccl", choices=["rccl", "host"],
                     help="--gpus N without a launcher: ncclGather over distinct devices, or host copies (ranks may share a GPU)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
@@ -107,8 +116,8 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="debug: gloo runs the N>1 path with host-side collectives and ranks sharing the visible GPUs")
     a = ap.parse_args()
-    if a.steps < 1 or a.warmup < 0 or a.cold_steps < 0 or a.gpus < 1:
-        ap.error("--steps and --gpus must be >= 1, --warmup and --cold-steps >= 0")
+    if a.steps < 1 or a.warmup < 0 or a.warm_steps < 0 or a.gpus < 1:
+        ap.error("--steps and --gpus must be >= 1, --warmup and --warm-steps >= 0")
     return a
 
 
@@ -191,7 +200,8 @@ def roofline(a, stats, kname, avg_ms, rows, workload, world):
     mem = {"achieved": round(achieved, 2), "unit": "GB/s", "bytes_per_launch": int(bytes_launch),
            "bytes_per_segment": round(bytes_launch / max(stats["segments"], 1), 2),
            "node_tests_per_segment": round(stats["node_tests"] / max(stats["segments"], 1), 3),
-           "prim_tests_per_segment": round(stats["prim_tests"] / max(stats["segments"], 1), 3)}
+           "prim_tests_per_segment": round(stats["prim_tests"] / max(stats["segments"], 1), 3),
+           "counted_by": stats.get("kernel")}  # the F_STATS twin of the timed variant (same traversal)
     if lds_variant(kname):
         mem.update(served_from="LDS", peak=round(LDS_PEAK_GBS, 1), frac=round(achieved / LDS_PEAK_GBS, 4))
         roof = {"bound": "lds", "achieved": mem["achieved"], "peak": mem["peak"], "unit": "GB/s", "frac": mem["frac"]}
@@ -303,14 +313,15 @@ def main():
     gathered = torch.empty(world * img.numel(), dtype=torch.uint8, device=cdev) if world > 1 else None
 
     seg_step = [0]
-    kms = []
+    kms, rms = [], []
     kname = [""]
     sched = []
 
     def step(args_):
         ctx.render_init(a.width, a.height, 1984)
         cnt = ctx.render(args_, fb.data_ptr())
-        kms.append(ctx.last_render_ms())
+        kms.append(ctx.last_kernel_ms())  # the render kernel alone (the roofline's launch duration)
+        rms.append(ctx.last_render_ms())   # probe + schedule + render kernel
         kname[0] = ctx.last_render_kernel()
         sched.append(ctx.last_render_schedule())
         ctx.resolve(args_, fb.data_ptr(), img.data_ptr())
@@ -331,56 +342,68 @@ def main():
             dist.barrier()
         return time.perf_counter() - t0
 
-    # module load + first allocations, on a tiny image (a different configuration: the schedule
-    # of the measured one stays cold)
+    # module load + first allocations, on a tiny image (a different configuration)
     ctx.render_init(64, 36, 1984)
     tiny = rt.make_args(64, 36, 1, 0, 1, a.depth, cam)
     tfb = torch.empty(64 * 36 * 3, dtype=torch.float32, device=dev)
     ctx.render(tiny, tfb.data_ptr())
-    # cold draws: nothing reused from an earlier launch (RT_FLAG_FRESH: each runs as the first draw
-    # of its configuration does -- probe launch, schedule from its estimate, render)
-    step(cold_args)
-    kms.clear()
-    sched.clear()
-    dt_cold = timed(max(1, a.cold_steps), cold_args) / max(1, a.cold_steps)
-    cold_kms = sum(kms) / len(kms)
-    assert all(x & (rt.RT_SCHED_PREVIOUS | rt.RT_SCHED_SPLIT_REPLAY) == 0 for x in sched), sched
-    cold_sched = sorted(set(sched))
 
     stats = None
-    if not a.no_stats:  # untimed pass of the counting variant: node / prim tests for B_seg
+    if not a.no_stats:  # untimed pass of the counting twin of the timed variant: node / prim tests for B_seg
         ctx.render_init(a.width, a.height, 1984)
         sargs = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, band_rows=a.band_rows,
-                             band_first=rank, band_stride=world, stats=True, exact=a.exact)
+                             band_first=rank, band_stride=world, stats=True, exact=a.exact, lds=not a.no_lds,
+                             step=not a.no_step, bins=not a.no_bins, schedule=False)
         stats = ctx.render(sargs, fb.data_ptr())
+        stats["kernel"] = ctx.last_render_kernel()
 
+    # warm leg (reported beside the value, never as it): two priming draws (the measuring one, the one
+    # recording split-sample states), then repeats that reuse both
+    dt_warm, warm_sched, warm_kms = None, [], None
+    if a.warm_steps > 0:
+        for _ in range(2):
+            step(args)
+        kms.clear()
+        rms.clear()
+        sched.clear()
+        dt_warm = timed(a.warm_steps, args) / a.warm_steps
+        warm_sched = sorted(set(sched))
+        warm_kms = sum(kms) / len(kms)
+
+    # the measured draws: one-shot (RT_FLAG_FRESH), W untimed then K timed -- last, so that a profile's
+    # last K render dispatches are the timed ones (scripts/pmc_summary.py PMC_LAST)
     for _ in range(a.warmup):
-        step(args)
+        step(cold_args)
     kms.clear()
+    rms.clear()
     sched.clear()
-    dt = timed(a.steps, args)
+    dt = timed(a.steps, cold_args)
+    assert all(x & (rt.RT_SCHED_PREVIOUS | rt.RT_SCHED_SPLIT_REPLAY) == 0 for x in sched), sched
 
     tot = torch.tensor([float(seg_step[0])], dtype=torch.float64, device=cdev)
-    tmax = torch.tensor([dt, dt_cold], dtype=torch.float64, device=cdev)
+    tmax = torch.tensor([dt, dt_warm or 0.0], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     segs = float(tot.item())
-    dt, dt_cold = float(tmax[0].item()), float(tmax[1].item())
+    dt, dt_warm = float(tmax[0].item()), (float(tmax[1].item()) if dt_warm is not None else None)
     value = segs * a.steps / dt / 1e6
 
     if rank == 0:
         avg_ms = sum(kms) / len(kms)
         workload = workload_name(a)
         roof = roofline(a, stats, kname[0], avg_ms, len(rows), workload, world)
-        extra = {"cold_ms_per_step": round(dt_cold * 1e3, 3), "cold_value": round(segs / dt_cold / 1e6, 2),
-                 "cold_kernel_ms": round(cold_kms, 3), "kernel_ms": round(avg_ms, 3),
+        extra = {"kernel_ms": round(avg_ms, 3), "render_call_ms": round(sum(rms) / len(rms), 3),
+                 "warm_value": round(segs / dt_warm / 1e6, 2) if dt_warm else None,
+                 "warm_ms_per_step": round(dt_warm * 1e3, 3) if dt_warm else None,
+                 "warm_kernel_ms": round(warm_kms, 3) if warm_kms else None,
                  "context_options": opts or "defaults",
-                 "schedule": "steady state: every timed draw repeats the configuration and reuses the item "
-                             "schedule (and split-sample states) of the draws before it; cold_* = draws that "
-                             "reuse nothing (RT_FLAG_FRESH), as a single draw() runs: probe launch, "
-                             "schedule from its estimate, render (bit 4 = probe-scheduled)",
-                 "timed_schedule_bits": sorted(set(sched)), "cold_schedule_bits": cold_sched,
+                 "schedule": "value: one-shot draws (RT_FLAG_FRESH) -- nothing reused from an earlier draw, "
+                             "each runs as a single draw() does: probe launch (bit 4), items ordered by its "
+                             "estimate, render; warm_*: repeats of the configuration that reuse the previous "
+                             "draw's measured item costs (bit 1) and recorded split-sample states (bit 2)",
+                 "timed_schedule_bits": sorted(set(sched)), "warm_schedule_bits": warm_sched,
+                 "stats_kernel": stats.get("kernel") if stats else None,
                  "driver": "torch.distributed (one process per GPU)" if world > 1 else "single process"}
         out = out_line(a, value, world, dt / a.steps, segs, roof, extra)
         if world == 1 and not a.no_cpu_baseline:
@@ -426,34 +449,37 @@ def main_inprocess(a):
     cold_args = rt.make_args(a.width, a.height, a.spp, 0, a.nfb, a.depth, cam, schedule=not a.no_schedule,
                              fresh=True, **kw)
     m.draw(rt.make_args(64, 36, 1, 0, 1, a.depth, cam, band_rows=4))  # module load on every device
-    m.draw(cold_args)
-    colds = []
-    for _ in range(max(1, a.cold_steps)):
-        t0 = time.perf_counter()
-        _, cnt, tm = m.draw(cold_args)
-        colds.append((time.perf_counter() - t0, tm))
+    warms = []
+    if a.warm_steps > 0:  # reported beside the value: repeats that reuse the schedule and split states
+        for _ in range(2):
+            m.draw(args)
+        for _ in range(a.warm_steps):
+            t0 = time.perf_counter()
+            _, cnt, tm = m.draw(args)
+            warms.append((time.perf_counter() - t0, tm))
     for _ in range(a.warmup):
-        m.draw(args)
-    warm = []
+        m.draw(cold_args)
+    colds = []
     t0 = time.perf_counter()
-    for _ in range(a.steps):  # each draw is synchronous: every rank's stream and the gather drained
-        img, cnt, tm = m.draw(args)
-        warm.append(tm)
+    for _ in range(a.steps):  # one-shot draws; each is synchronous: every rank's stream and the gather drained
+        img, cnt, tm = m.draw(cold_args)
+        colds.append(tm)
     dt = time.perf_counter() - t0
     segs = cnt["segments"]
     value = segs * a.steps / dt / 1e6
-    dt_cold = sum(x[0] for x in colds) / len(colds)
-    per_rank_k = [round(sum(t["kernel_ms"][r] for t in warm) / len(warm), 3) for r in range(a.gpus)]
-    per_rank_cold = [round(sum(t[1]["kernel_ms"][r] for t in colds) / len(colds), 3) for r in range(a.gpus)]
-    extra = {"cold_ms_per_step": round(dt_cold * 1e3, 3), "cold_value": round(segs / dt_cold / 1e6, 2),
-             "kernel_ms_per_rank": per_rank_k, "cold_kernel_ms_per_rank": per_rank_cold,
-             "render_ms_max": round(sum(t["render_ms_max"] for t in warm) / len(warm), 3),
-             "gather_ms": round(sum(t["gather_ms"] for t in warm) / len(warm), 3),
-             "gather_bytes": warm[-1]["gather_bytes"], "warm": warm[-1]["warm"],
-             "schedule": "steady state: every timed draw repeats the configuration and reuses the item "
-                         "schedule (and split-sample states) of the draws before it; cold_* = draws that "
-                         "reuse nothing (RT_FLAG_FRESH), as a single draw() runs: probe launch, "
-                         "schedule from its estimate, render",
+    dt_warm = sum(x[0] for x in warms) / len(warms) if warms else None
+    per_rank_k = [round(sum(t["kernel_ms"][r] for t in colds) / len(colds), 3) for r in range(a.gpus)]
+    per_rank_warm = ([round(sum(t[1]["kernel_ms"][r] for t in warms) / len(warms), 3) for r in range(a.gpus)]
+                     if warms else None)
+    extra = {"warm_ms_per_step": round(dt_warm * 1e3, 3) if dt_warm else None,
+             "warm_value": round(segs / dt_warm / 1e6, 2) if dt_warm else None,
+             "kernel_ms_per_rank": per_rank_k, "warm_kernel_ms_per_rank": per_rank_warm,
+             "render_ms_max": round(sum(t["render_ms_max"] for t in colds) / len(colds), 3),
+             "gather_ms": round(sum(t["gather_ms"] for t in colds) / len(colds), 3),
+             "gather_bytes": colds[-1]["gather_bytes"], "warm": colds[-1]["warm"],
+             "schedule": "value: one-shot draws (RT_FLAG_FRESH), nothing reused from an earlier draw; warm_*: "
+                         "repeats of the configuration that reuse the previous draw's item costs and "
+                         "recorded split-sample states",
              "driver": f"librt_multi.so in one process, {a.gpus} ranks on devices {devices}, "
                        f"gather {'ncclGather (RCCL)' if mode == multi.RT_GATHER_RCCL else 'host copies'}; "
                        "a step includes the copy of the assembled image to the host"}

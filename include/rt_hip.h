@@ -233,7 +233,8 @@ enum rt_merge_order {
 typedef struct rt_ctx_options {
   /* upload time (rt_scene_upload) */
   int32_t world_tree;        /* 1: a list world flattened into ONE traversal tree for the stepwise
-                                kernel (measured slower than the merged search; default 0)         */
+                                kernel (measured slower than the merged search; default 0).  This
+                                and the other 0/1 fields reject any other value                    */
   int32_t quantized_tree;    /* 1: the world BVH's traversal tree as 24-byte records in LDS when it
                                 fits (C4's mesh; default 1)                                         */
   int32_t merged_search;     /* rt_merge_mode (default RT_MERGE_ON)                                */
@@ -249,7 +250,8 @@ typedef struct rt_ctx_options {
                                 0 = the share-size rule (default)                                   */
   int32_t split_order;       /* 1: split samples and unsplit items claimed in one longest-first
                                 sequence (default); 0: split samples first, in item order          */
-  int32_t cost_shift;        /* item-schedule cost buckets of 2^cost_shift segments; -1 = automatic */
+  int32_t cost_shift;        /* item-schedule cost buckets of 2^cost_shift segments, 0..12; -1 =
+                                automatic                                                           */
   float long_pct;            /* share of the longest items whose waves run at raised priority
                                 (default 2)                                                         */
   int32_t probe_schedule;    /* k > 0: the first launch of a configuration (>= 4 samples per pixel,
@@ -282,8 +284,12 @@ int rt_read_states(rt_ctx* ctx, int64_t first, int64_t count, uint32_t* out);
  * buffers are rendered into a temporary device buffer and copied back before the call returns.
  * counters may be NULL. */
 int rt_render(rt_ctx* ctx, const rt_render_args* args, float* fb, rt_counters* counters);
-/* Duration in ms of the last render kernel, from HIP events recorded on the context stream. */
+/* Device time in ms of the last rt_render call, from HIP events recorded on the context stream: a first
+ * launch's probe launch and item schedule (RT_SCHED_PROBE) included, the host staging of a host fb
+ * excluded. */
 float rt_last_render_ms(const rt_ctx* ctx);
+/* ... of its render kernel alone (with the split-sample merge after it, RT_SCHED_SPLIT_REPLAY). */
+float rt_last_kernel_ms(const rt_ctx* ctx);
 /* Kernel of the last render launch as rocprof names it (stem, e.g. "render_step_kernel<25730>"):
  * the kernel variant the context picked for the scene's features and flags. */
 const char* rt_last_render_kernel(const rt_ctx* ctx);

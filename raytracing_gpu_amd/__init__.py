@@ -139,6 +139,7 @@ ABI = {
     "rt_read_states": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
     "rt_render": (c_int, [c_void_p, POINTER(rt_render_args), c_void_p, POINTER(rt_counters)]),
     "rt_last_render_ms": (c_float, [c_void_p]),
+    "rt_last_kernel_ms": (c_float, [c_void_p]),
     "rt_last_render_kernel": (ctypes.c_char_p, [c_void_p]),
     "rt_last_render_schedule": (c_int32, [c_void_p]),
     "rt_audit_log": (c_int, [c_void_p, POINTER(c_float), c_int32]),
@@ -368,7 +369,12 @@ class Context:
                     "rt_resolve")
 
     def last_render_ms(self) -> float:
+        """Device time of the last render call (a first launch's probe and schedule included)."""
         return float(lib().rt_last_render_ms(self._c))
+
+    def last_kernel_ms(self) -> float:
+        """Device time of the last render call's render kernel alone (rocprof's duration of it)."""
+        return float(lib().rt_last_kernel_ms(self._c))
 
     def last_render_kernel(self) -> str:
         """rocprof name stem of the kernel the last render launched."""

@@ -18,7 +18,9 @@ EXAMPLES = os.path.join(ROOT, "examples")
 RT_MAIN = os.path.join(EXAMPLES, "bin", "rt_main")
 
 HIP_SOURCES = ["rt_kernels.hip", "rt_scene.cpp", "rt_obj.cpp", "rt_image.cpp"]
-HIP_DEPS = HIP_SOURCES + ["rt_detmath.h", "rt_xorwow.h", "rt_host_geom.h"]
+# every header of csrc/ (rt_diag.h included): an edit to any of them rebuilds the library and changes
+# kernel_build_id() (tests/test_build_cpu.py checks that each local #include is covered)
+HIP_DEPS = HIP_SOURCES + sorted(f for f in os.listdir(CSRC) if f.endswith(".h"))
 # -ffp-contract=off: no FMA contraction anywhere, so every float op rounds like the reference's
 # C++ source and like the CPU oracle; fp32 div/sqrt correctly rounded (IEEE) on the device.
 HIPCC_FLAGS = [

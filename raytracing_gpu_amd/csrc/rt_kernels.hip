@@ -67,6 +67,8 @@ enum : int {
   F_WORLD = 1 << 15,  // list world flattened into ONE traversal tree (render_step_kernel; rt_scene_upload)
   F_QLDS = 1 << 16,   // the world BVH's traversal tree quantized to 24-byte pair records in LDS (qpair)
   F_MERGE = 1 << 17,  // render_kernel answers world queries with world_search only (merge_ok scenes)
+  F_PROBE = 1 << 18,  // the same code under its own symbol for the probe launches of a first launch
+                      // (rt_render): rocprof then times the render launches apart from the probes
   F_ALL = (1 << 11) - 2,
   F_SPHERES = F_MOVING | F_CHECKER | F_BVH,           // basic, first, big1 (C2), two_spheres
   F_CORNELL = F_RECT | F_LIST | F_XFORM | F_MEDIUM,   // cornell, cornell_smoke (C3)
@@ -2922,7 +2924,7 @@ struct rt_ctx {
   int device = 0;
   rt_ctx_options opt{};  // rt_ctx_set_options (defaults: rt_ctx_options_default)
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;  // render call start, its end; render kernel start
   std::string err;
   std::vector<void*> scene_bufs;
   DScene scene{};
@@ -2988,7 +2990,8 @@ struct rt_ctx {
   bool world_tree = false;  // a list world flattened into the world tree (render_step_kernel<..|F_WORLD>)
   int dev_nodes = 0, dev_prims = 0, dev_mats = 0, dev_texs = 0, dev_imgs = 0;  // device array sizes (LDS staging)
   int plane_fb = -1, plane_pairs = 0;  // world tree staged in planes by the stepwise LDS variant (-1: not)
-  float last_ms = 0.0f;
+  float last_ms = 0.0f;         // the last rt_render's device time: probe + schedule + render kernel
+  float last_kernel_ms = 0.0f;  // ... its render kernel (and split merge) alone
   int last_sched = 0;  // RT_SCHED_* of the last render launch
   char last_kernel[48] = "";  // rocprof name stem of the last render launch, e.g. render_step_kernel<25730>
   float* dbg = nullptr;  // audit log: [0] = count, then 16 floats per entry
@@ -3043,6 +3046,13 @@ const Variant kVariants[] = {
     RT_VARIANT(F_MESH | F_EXACT),
     RT_VARIANT(F_FINAL),
     RT_VARIANT(F_FINAL | F_MERGE),
+    // the counting twin of C2's stepwise LDS variant: bench.py's untimed stats pass counts the node and
+    // primitive tests of the traversal it times (culled search, camera tile lists)
+    RT_VARIANT_STEP(F_SPHERES | F_LDS | F_STEP | F_STATS),
+    // probe twins of the product variants of C2, C4 and C5 (F_PROBE changes no code)
+    RT_VARIANT_STEP(F_SPHERES | F_LDS | F_STEP | F_PROBE),
+    RT_VARIANT_STEP(F_MESH | F_STEP | F_QLDS | F_PROBE),
+    RT_VARIANT(F_FINAL | F_MERGE | F_PROBE),
 };
 #undef RT_VARIANT
 #undef RT_VARIANT_STEP
@@ -3059,7 +3069,7 @@ int pick_variant(int features, bool stats, bool exact, bool check, bool lds, boo
     int best = -1;
     for (int v = 0; v < kNumVariants; ++v) {
       const int m = kVariants[v].mask;
-      if ((m & modes) != want || (features & ~m) != 0) continue;
+      if ((m & modes) != want || (features & ~m) != 0 || (m & F_PROBE) != 0) continue;
       const int pm = __builtin_popcount(m), pb = best < 0 ? 0 : __builtin_popcount(kVariants[best].mask);
       if (best < 0 || (widest ? pm > pb : pm < pb)) best = v;
     }
@@ -3084,6 +3094,15 @@ int pick_variant(int features, bool stats, bool exact, bool check, bool lds, boo
   if (v >= 0 && merge && mode == 0)  // its merged-search twin (render_kernel; merge_ok scenes)
     for (int w = 0; w < kNumVariants; ++w)
       if (kVariants[w].mask == (kVariants[v].mask | F_MERGE)) return w;
+  if (v >= 0 && mode == F_STATS && lds && step && !world)  // the counting twin of the stepwise LDS variant
+    for (int w = 0; w < kNumVariants; ++w)
+      if (kVariants[w].mask == (kVariants[v].mask | F_LDS | F_STEP)) return w;
+  return v;
+}
+// The probe twin of variant v (same code, own symbol), or v itself when none is compiled.
+int probe_variant(int v) {
+  for (int w = 0; w < kNumVariants; ++w)
+    if (kVariants[w].mask == (kVariants[v].mask | F_PROBE)) return w;
   return v;
 }
 int variant_block(int v) { return (kVariants[v].mask & (F_LDS | F_QLDS)) != 0 ? 1024 : 256; }
@@ -3565,6 +3584,7 @@ int rt_ctx_create(int hip_device, rt_ctx** out) {
   if (rc == RT_OK) chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
   if (rc == RT_OK) chk(hipEventCreate(&c->ev0), "hipEventCreate");
   if (rc == RT_OK) chk(hipEventCreate(&c->ev1), "hipEventCreate");
+  if (rc == RT_OK) chk(hipEventCreate(&c->ev2), "hipEventCreate");
   if (rc == RT_OK) chk(hipMalloc((void**)&c->work, 8 * sizeof(unsigned long long)), "hipMalloc");
   if (rc == RT_OK) {
     std::vector<uint32_t> seq(32 * 800);
@@ -3634,6 +3654,7 @@ int rt_ctx_destroy(rt_ctx* c) {
   if (c->cam_st) (void)hipFree(c->cam_st);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev2) (void)hipEventDestroy(c->ev2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -3664,8 +3685,10 @@ int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
   if (o->merged_search < RT_MERGE_ON || o->merged_search > RT_MERGE_FALLBACK_ALL ||
       o->merge_order < RT_ORDER_DISTANCE || o->merge_order > RT_ORDER_REVERSED || o->shade_min < 0 ||
       o->shade_min > 64 || !(o->bins_min_items_per_lane >= 0.0f) || !(o->split_min_segments >= 0.0f) ||
-      o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f) || o->probe_schedule < -1 ||
-      o->probe_schedule > 64 || !(o->probe_max_items_per_lane >= 0.0f))
+      o->cost_shift < -1 || o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f) ||
+      o->probe_schedule < -1 || o->probe_schedule > 64 || !(o->probe_max_items_per_lane >= 0.0f) ||
+      (o->world_tree & ~1) != 0 || (o->quantized_tree & ~1) != 0 || (o->dedup_triangles & ~1) != 0 ||
+      (o->split_order & ~1) != 0)
     return fail(c, RT_ERR_ARG, "bad context options");
   c->opt = *o;
   // the schedule and split thresholds come from the options: every configuration starts cold again
@@ -4189,7 +4212,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_soa* s) {
   }
   c->dev_nodes = (int)nodes.size();
   // the stepwise LDS variant stages the world BVH's traversal tree in planes (stage_lds): it must be
-  // the last tree of the node array and have at most kPlanePairs records
+  // the last tree of the node array and have at most kPlanePairs records.  A larger sphere tree (more
+  // than 512 primitives) runs the stepwise kernel from global memory instead (documented cap: the
+  // plane offsets are immediates, and every reference sphere scene fits; C2 has 487 pairs)
   c->plane_fb = -1;
   if (world_step) {
     const rt_object& wo = objects[(size_t)s->world[0]];
@@ -4656,7 +4681,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     Q.row_cost = nullptr;
     Q.split_mode = 0;
     void* qargs[] = {&Q};
-    HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), qargs, shmem, c->stream));
+    HIPCHK(c, hipLaunchKernel(kVariants[probe_variant(var)].fn, dim3(blocks), dim3(bs), qargs, shmem, c->stream));
     HIPCHK(c, hipGetLastError());
     probe_smooth_kernel<<<(unsigned)((pitems + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
         c->probe_cost, c->probe_cost + pitems, prow, pw);
@@ -4665,6 +4690,13 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
         c->probe_cost + pitems, c->item_cost, (unsigned long long)items, a->width, a->fb_count, a->spp, ps, pw);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemsetAsync(c->work, 0, 8 * sizeof(unsigned long long), c->stream));
+    // The probe's schedule overwrites the context's one (perm, long prefix, split items): whatever
+    // configuration perm_key named no longer has its schedule, so it runs cold again when it repeats
+    // (A, A, probe of B, A must not claim A's items through B's perm).
+    std::fill(c->perm_key, c->perm_key + K, -1LL);
+    c->split_state = -1;
+    c->n_split = 0;
+    c->order_ok = false;
     if ((rc = build_schedule(c, items, a->spp, 0ull))) return rc;
     P.perm = c->perm;
     P.n_long = c->n_long;
@@ -4673,6 +4705,8 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   RT_STAMP_HOST_RESET();
   RT_WAVE_HOST_RESET();
   void* kargs[] = {&P};
+  // rt_last_kernel_ms: the render kernel (and the split merge), not the probe before it
+  HIPCHK(c, hipEventRecord(c->ev2, c->stream));
   HIPCHK(c, hipLaunchKernel(kVariants[var].fn, dim3(blocks), dim3(bs), kargs, shmem, c->stream));
   HIPCHK(c, hipGetLastError());
   if (split_mode == 2) {
@@ -4706,6 +4740,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     c->split_seed = a->seed;
   }
   HIPCHK(c, hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1));
+  HIPCHK(c, hipEventElapsedTime(&c->last_kernel_ms, c->ev2, c->ev1));
   if (counters) {
     counters->segments = host_cnt[1];
     counters->node_tests = host_cnt[2];
@@ -4723,6 +4758,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
 }  // namespace
 
 float rt_last_render_ms(const rt_ctx* c) { return c ? c->last_ms : 0.0f; }
+float rt_last_kernel_ms(const rt_ctx* c) { return c ? c->last_kernel_ms : 0.0f; }
 const char* rt_last_render_kernel(const rt_ctx* c) { return c ? c->last_kernel : ""; }
 int32_t rt_last_render_schedule(const rt_ctx* c) { return c ? c->last_sched : 0; }
 

@@ -15,7 +15,7 @@ sys.path.insert(0, ROOT)
 from raytracing_gpu_amd import _build  # noqa: E402
 
 FEAT = {0: "STATS", 1: "MOVING", 2: "RECT", 3: "TRI", 4: "LIST", 5: "XFORM", 6: "MEDIUM", 7: "CHECKER", 8: "NOISE",
-        9: "IMAGE", 10: "BVH", 11: "EXACT", 12: "CHECK", 13: "LDS", 14: "STEP", 15: "WORLD", 16: "QLDS", 17: "MERGE"}
+        9: "IMAGE", 10: "BVH", 11: "EXACT", 12: "CHECK", 13: "LDS", 14: "STEP", 15: "WORLD", 16: "QLDS", 17: "MERGE", 18: "PROBE"}
 NAMED = {25730: "C2 (SPHERES|LDS|STEP)", 1112: "C3 (CORNELL)", 1560: "C4 (MESH)", 1918: "C5 entry loop", 132990: "C5 (FINAL|MERGE)", 49268: "C3 world", 51070: "C5 world", 83480: "C4 quantized LDS",
          2046: "ALL"}
 
