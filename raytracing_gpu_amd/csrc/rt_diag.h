@@ -9,8 +9,9 @@
 //      (scripts/diag_stamps.py)
 //   4  per-wave start / work-exhausted / end times (s_memrealtime), written to $RT_WAVE_TIMES_OUT
 //      (scripts/diag_waves.py)
-//   8  every measuring launch's per-item segment counts, written to $RT_ITEM_COST_OUT
-//      (scripts/diag_pace.py)
+//   8  every measuring launch's per-item segment counts, written to $RT_ITEM_COST_OUT, and every probe
+//      launch's raw per-grid-point counts, written to $RT_PROBE_OUT (scripts/diag_pace.py,
+//      scripts/diag_order.py)
 // Bits 2 and 4 perturb the timing they measure; use one at a time.
 #pragma once
 
@@ -176,6 +177,20 @@ __device__ __forceinline__ unsigned long long rt_realtime() {
       }                                                                                               \
     }                                                                                                 \
   } while (0)
+#define RT_DIAG_PROBE_COSTS(c, n)                                                                     \
+  do {                                                                                                \
+    if (const char* p_ = getenv("RT_PROBE_OUT")) {                                                    \
+      std::vector<uint16_t> pc_((size_t)(n));                                                         \
+      HIPCHK(c, hipMemcpyAsync(pc_.data(), (c)->probe_cost, pc_.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, \
+                               (c)->stream));                                                         \
+      HIPCHK(c, hipStreamSynchronize((c)->stream));                                                   \
+      if (FILE* f_ = fopen(p_, "wb")) {                                                               \
+        fwrite(pc_.data(), sizeof(uint16_t), pc_.size(), f_);                                         \
+        fclose(f_);                                                                                   \
+      }                                                                                               \
+    }                                                                                                 \
+  } while (0)
 #else
 #define RT_DIAG_ITEM_COSTS(c, items)
+#define RT_DIAG_PROBE_COSTS(c, n)
 #endif

@@ -3423,8 +3423,9 @@ int sort_scatter(rt_ctx* c, long long n, const unsigned* base, uint32_t* out) {
   return RT_OK;
 }
 
-// Mean of the probe counts within kProbeRadius grid points (rows and pixels, clipped at the edges):
-// one sample's count is a noisy estimate of a pixel's cost, a neighbourhood's mean is a steadier one.
+// Mean of the probe counts within kProbeRadius grid points (rows and pixels, clipped at the edges), in
+// 1/16 segment: one sample's count is a noisy estimate of a pixel's cost, a neighbourhood's mean is a
+// steadier one.
 // Measured (MI355X, one GPU rendering each rank's share, first launches, median of 3; probe of every
 // pixel), cold share ms at N = 4 / 8: C2 10 x 10 no probe 5.87 / 4.17, radius 0 7.02 / 5.10, 2 5.64 /
 // 4.02, 5 5.65 / 4.12; C4 no probe 32.86 / 26.70, radius 0 28.14 / 27.87, 2 27.49 / 27.08, 5 25.58 /
@@ -3446,21 +3447,31 @@ __global__ __launch_bounds__(kBlock) void probe_smooth_kernel(const uint16_t* __
       ++n;
     }
   }
-  out[k] = (uint16_t)((sum + n / 2) / n);
+  out[k] = (uint16_t)((16 * sum + n / 2) / n);
 }
 
-// Probe estimate of every item: the (smoothed) probe count of its grid point (sample 0 of the first fb at row
-// position ps * (q / ps), pixel ps * (i / ps)) times spp.  Items are row-major with the fb inside the
-// row (render kernels); the probe launch's items are the grid's (row position, pixel) points.
-__global__ __launch_bounds__(kBlock) void probe_expand_kernel(const uint16_t* __restrict__ probe,
-                                                              uint16_t* __restrict__ cost, unsigned long long items,
-                                                              int W, int fbc, int spp, int ps, int pw) {
+// Sort key of every item from the probe: the smoothed probe count (1/16 segment) of its grid point (sample
+// 0 of the first fb at row position ps * (q / ps), pixel ps * (i / ps)) times spp, in cost buckets of
+// 2^shift segments, clamped to 255.  Items are row-major with the fb inside the row (render kernels); the
+// probe launch's items are the grid's (row position, pixel) points.
+__global__ __launch_bounds__(kBlock) void probe_keys_kernel(const uint16_t* __restrict__ probe, uint8_t* __restrict__ key,
+                                                            unsigned long long items, int W, int fbc, int spp, int ps,
+                                                            int pw, int shift) {
   const unsigned long long per_row = (unsigned long long)fbc * (unsigned)W;
   for (unsigned long long k = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; k < items;
        k += (unsigned long long)gridDim.x * blockDim.x) {
     const unsigned long long q = k / per_row, i = (k - q * per_row) % (unsigned)W;
-    const unsigned v = (unsigned)probe[(q / (unsigned)ps) * (unsigned)pw + i / (unsigned)ps] * (unsigned)spp;
-    cost[k] = (uint16_t)(v < 65535u ? v : 65535u);
+    const unsigned long long v = (unsigned long long)probe[(q / (unsigned)ps) * (unsigned)pw + i / (unsigned)ps] * spp;
+    key[k] = (uint8_t)min(255ull, v >> (4 + shift));
+  }
+}
+// Bases of a descending counting sort from its key totals: base[v] = keys above v (one lane: 256 adds).
+__global__ __launch_bounds__(64) void key_base_kernel(const unsigned* __restrict__ total, unsigned* __restrict__ base) {
+  if (threadIdx.x != 0) return;
+  unsigned acc = 0;
+  for (int v = 255; v >= 0; --v) {
+    base[v] = acc;
+    acc += total[v];
   }
 }
 
@@ -3553,6 +3564,35 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
       for (long long v = 0; v < key; ++v) c->rest_gt[(size_t)v] += (unsigned)hist[(size_t)b];
     }
   }
+  return RT_OK;
+}
+
+// Item schedule of a probe-scheduled first launch from the smoothed probe grid (c->probe_cost + pitems):
+// every step on the device, no host round trip (the draw's critical path): per-item keys, the tile
+// histograms and their scan, the bases, the stable scatter into perm.  The long prefix is the first
+// long_pct % of the positions.  Cost buckets of 8 segments, as the measured schedule's (natural order
+// inside a bucket keeps neighbouring claims coherent), wider where smoothed means of up to 32 segments
+// per sample would saturate the top bucket (a grid point above that, rare, saturates it).
+int probe_schedule(rt_ctx* c, long long items, int spp, int width, int fbc, int ps, int pw, long long pitems) {
+  uint8_t* keys = sort_keys(c, items);
+  if (!keys) return fail(c, RT_ERR_HIP, "out of device memory (probe schedule)");
+  int shift = 3;
+  while (shift < 12 && ((32LL * spp) >> shift) > 255) ++shift;
+  if (c->opt.cost_shift >= 0) shift = c->opt.cost_shift;  // tuning
+  probe_keys_kernel<<<(unsigned)std::min<long long>(4096, (items + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
+      c->probe_cost + pitems, keys, (unsigned long long)items, width, fbc, spp, ps, pw, shift);
+  HIPCHK(c, hipGetLastError());
+  const unsigned tiles = (unsigned)((items + kOrderTile - 1) / kOrderTile);
+  unsigned* tile_tab = (unsigned*)(c->sort_scratch + ((items + 255) & ~255LL));
+  unsigned* totals = c->order_tab + 256 + 2 * kOrderKeys;
+  order_tile_hist_kernel<<<tiles, 64, 0, c->stream>>>(keys, (unsigned long long)items, tile_tab);
+  HIPCHK(c, hipGetLastError());
+  order_scan_kernel<<<256, 256, 0, c->stream>>>(tile_tab, tiles, totals);
+  HIPCHK(c, hipGetLastError());
+  key_base_kernel<<<1, 64, 0, c->stream>>>(totals, c->order_tab);
+  HIPCHK(c, hipGetLastError());
+  if (int rc = sort_scatter(c, items, c->order_tab, c->perm)) return rc;
+  c->n_long = (unsigned long long)((double)items * c->opt.long_pct / 100.0);
   return RT_OK;
 }
 
@@ -3678,6 +3718,7 @@ void rt_ctx_options_default(rt_ctx_options* o) {
   o->long_pct = 2.0f;
   o->probe_schedule = -1;
   o->probe_max_items_per_lane = 0.0f;
+  o->probe_depth = 0;
 }
 
 int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
@@ -3688,7 +3729,7 @@ int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
       o->cost_shift < -1 || o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f) ||
       o->probe_schedule < -1 || o->probe_schedule > 64 || !(o->probe_max_items_per_lane >= 0.0f) ||
       (o->world_tree & ~1) != 0 || (o->quantized_tree & ~1) != 0 || (o->dedup_triangles & ~1) != 0 ||
-      (o->split_order & ~1) != 0)
+      (o->split_order & ~1) != 0 || o->probe_depth < 0)
     return fail(c, RT_ERR_ARG, "bad context options");
   c->opt = *o;
   // the schedule and split thresholds come from the options: every configuration starts cold again
@@ -4672,6 +4713,9 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     RenderParams Q = P;
     Q.spp = 1;
     Q.fb_count = 1;
+    // a probe sample's path is cut after probe_depth segments: the launch (one sample per lane) lasts as
+    // long as its longest path, and the estimate needs only the short ones' counts to rank regions
+    if (c->opt.probe_depth > 0) Q.max_depth = std::min(a->max_depth, c->opt.probe_depth);
     Q.total_items = (unsigned long long)pitems;
     Q.pstep = ps;
     Q.per_row = pw;
@@ -4683,11 +4727,9 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     void* qargs[] = {&Q};
     HIPCHK(c, hipLaunchKernel(kVariants[probe_variant(var)].fn, dim3(blocks), dim3(bs), qargs, shmem, c->stream));
     HIPCHK(c, hipGetLastError());
+    RT_DIAG_PROBE_COSTS(c, pitems);  // diagnostic builds only (rt_diag.h): the raw probe counts to a file
     probe_smooth_kernel<<<(unsigned)((pitems + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
         c->probe_cost, c->probe_cost + pitems, prow, pw);
-    HIPCHK(c, hipGetLastError());
-    probe_expand_kernel<<<(unsigned)std::min<long long>(4096, (items + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
-        c->probe_cost + pitems, c->item_cost, (unsigned long long)items, a->width, a->fb_count, a->spp, ps, pw);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemsetAsync(c->work, 0, 8 * sizeof(unsigned long long), c->stream));
     // The probe's schedule overwrites the context's one (perm, long prefix, split items): whatever
@@ -4697,7 +4739,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     c->split_state = -1;
     c->n_split = 0;
     c->order_ok = false;
-    if ((rc = build_schedule(c, items, a->spp, 0ull))) return rc;
+    if ((rc = probe_schedule(c, items, a->spp, a->width, a->fb_count, ps, pw, pitems))) return rc;
     P.perm = c->perm;
     P.n_long = c->n_long;
   }

@@ -10,10 +10,10 @@ for rep in $(seq 1 ${REPS:-2}); do
   for pair in "$@"; do
     name=${pair%%=*}; lib=${pair#*=}
     log=gpurun_out/ab_${tag}_${name}_$rep.log
-    RT_HIP_LIB=$lib timeout -k 10 300 python -u bench.py $args --steps ${STEPS_AB:-5} --warmup 2 --cold-steps 1 \
+    RT_HIP_LIB=$lib timeout -k 10 300 python -u bench.py $args --steps ${STEPS_AB:-5} --warmup 2 --warm-steps 2 \
       --no-cpu-baseline --no-stats ${AB_ARGS:-} > $log 2>&1
     rc=$?
-    echo "$tag $name #$rep rc=$rc $(grep -o '"value": [0-9.]*\|"kernel_ms": [0-9.]*\|"cold_kernel_ms": [0-9.]*' $log | tr '\n' ' ')"
+    echo "$tag $name #$rep rc=$rc $(grep -o '"value": [0-9.]*\|"kernel_ms": [0-9.]*\|"warm_kernel_ms": [0-9.]*' $log | tr '\n' ' ')"
     case $rc in 0) ;; *) exit $rc;; esac
   done
 done

@@ -6,6 +6,6 @@ set -u
 mkdir -p gpurun_out
 tag=$1; args=$2; shift 2
 for rep in $(seq 1 ${REPS:-2}); do for o in "$@"; do
-  timeout -k 10 300 python -u bench.py $args --steps ${STEPS_AB:-5} --warmup 2 --cold-steps 1 --no-cpu-baseline --no-stats $(echo ",$o" | sed 's/,/ --opt /g') > gpurun_out/sw_${tag}_${o//[=.,]/_}_$rep.log 2>&1 || exit $?
-  echo "$tag $o #$rep $(grep -o '"value": [0-9.]*\|"kernel_ms": [0-9.]*\|"cold_kernel_ms": [0-9.]*' gpurun_out/sw_${tag}_${o//[=.,]/_}_$rep.log | tr '\n' ' ')"
+  timeout -k 10 300 python -u bench.py $args --steps ${STEPS_AB:-5} --warmup 2 --warm-steps 2 --no-cpu-baseline --no-stats $(echo ",$o" | sed 's/,/ --opt /g') > gpurun_out/sw_${tag}_${o//[=.,]/_}_$rep.log 2>&1 || exit $?
+  echo "$tag $o #$rep $(grep -o '"value": [0-9.]*\|"kernel_ms": [0-9.]*\|"warm_kernel_ms": [0-9.]*' gpurun_out/sw_${tag}_${o//[=.,]/_}_$rep.log | tr '\n' ' ')"
 done; done

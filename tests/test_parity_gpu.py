@@ -468,7 +468,7 @@ def test_bench_inprocess_two_ranks_match_one(tmp_path):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    common = ["bench.py", "--steps", "1", "--warmup", "1", "--cold-steps", "1", "--no-cpu-baseline",
+    common = ["bench.py", "--steps", "1", "--warmup", "1", "--warm-steps", "1", "--no-cpu-baseline",
               "--no-stats", "--width", "200", "--height", "112", "--spp", "2", "--nfb", "2"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.pop("WORLD_SIZE", None)
@@ -481,7 +481,7 @@ def test_bench_inprocess_two_ranks_match_one(tmp_path):
     assert two.returncode == 0, two.stderr[-2000:]
     line = json.loads([x for x in two.stdout.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 2 and "librt_multi.so" in line["driver"]
-    assert line["value"] > 0 and line["cold_ms_per_step"] > 0
+    assert line["value"] > 0 and line["warm_ms_per_step"] > 0
     assert (tmp_path / "n1.png").read_bytes() == (tmp_path / "n2.png").read_bytes()
 
 

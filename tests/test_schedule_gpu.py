@@ -87,7 +87,7 @@ def test_bad_options_are_rejected(rtlib, gpu_ctx):
         assert gpu_ctx.options() == before, bad
 
 
-def test_scheduled_launch_beyond_64m_items(rtlib, gpu_ctx):
+def test_scheduled_launch_beyond_64m_items(rtlib, gpu_ctx, ctx_opts):
     """Round-5 verdict item 4a: a launch of more than 64 M items through its item schedule (32-bit perm
     positions; the limit is 2^31 items): big1 at 1200x800 as 70 fb x 2 spp (67.2 M items, fb ids up to
     69, slot products up to 70 * 960 000).  The probe-scheduled first launch, the scheduled second
@@ -98,6 +98,9 @@ def test_scheduled_launch_beyond_64m_items(rtlib, gpu_ctx):
 
     W, H, spp, nfb = 1200, 800, 2, 70
     assert nfb * W * H > 64 * 2**20
+    # at 256 items per lane the share rule splits nothing: split the items of >= 16 segments (millions of
+    # split samples, 32-bit claim positions past 64 M)
+    ctx_opts(split_min_segments=16.0)
     gpu_ctx.upload(rtlib.Scene.builtin("big1"))
     n = nfb * H * W * 3
 
