@@ -263,7 +263,8 @@ typedef struct rt_ctx_options {
   float probe_max_items_per_lane; /* > 0: probe only launches with fewer items per resident lane (a
                                 multi-GPU share); 0 (default): any launch                           */
   int32_t probe_depth;       /* k > 0: a probe sample's path ends after k segments (the probe launch
-                                lasts as long as its longest path); 0: the launch's max_depth       */
+                                lasts as long as its longest path); 0: the launch's max_depth; -1
+                                (default): 10 for the stepwise kernel, 20 for the others            */
 } rt_ctx_options;
 void rt_ctx_options_default(rt_ctx_options* opts);
 int rt_ctx_set_options(rt_ctx* ctx, const rt_ctx_options* opts);

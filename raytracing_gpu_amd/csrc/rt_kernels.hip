@@ -3718,7 +3718,7 @@ void rt_ctx_options_default(rt_ctx_options* o) {
   o->long_pct = 2.0f;
   o->probe_schedule = -1;
   o->probe_max_items_per_lane = 0.0f;
-  o->probe_depth = 0;
+  o->probe_depth = -1;
 }
 
 int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
@@ -3729,7 +3729,7 @@ int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
       o->cost_shift < -1 || o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f) ||
       o->probe_schedule < -1 || o->probe_schedule > 64 || !(o->probe_max_items_per_lane >= 0.0f) ||
       (o->world_tree & ~1) != 0 || (o->quantized_tree & ~1) != 0 || (o->dedup_triangles & ~1) != 0 ||
-      (o->split_order & ~1) != 0 || o->probe_depth < 0)
+      (o->split_order & ~1) != 0 || o->probe_depth < -1)
     return fail(c, RT_ERR_ARG, "bad context options");
   c->opt = *o;
   // the schedule and split thresholds come from the options: every configuration starts cold again
@@ -4714,8 +4714,14 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     Q.spp = 1;
     Q.fb_count = 1;
     // a probe sample's path is cut after probe_depth segments: the launch (one sample per lane) lasts as
-    // long as its longest path, and the estimate needs only the short ones' counts to rank regions
-    if (c->opt.probe_depth > 0) Q.max_depth = std::min(a->max_depth, c->opt.probe_depth);
+    // long as its longest path, and the estimate needs only the short ones' counts to rank regions.
+    // Automatic (-1): 10 for the stepwise kernel, 20 for render_kernel.  Measured (MI355X, one GPU
+    // rendering every rank's share, first launches, ms at N = 1 / 4 / 8; profiles/r06/probe_depth/):
+    // C2 full depth 16.94 / 5.66 / 4.08, 10: 16.71 / 5.68 / 3.97, 6: 16.68 / 5.69 / 4.25; C4 full
+    // 66.25 / 26.55 / 25.71, 10: 65.61 / 25.25 / 24.34, 16: 65.42 / 25.77 / 25.19; C5 full 64.26 /
+    // 22.65 / 15.36, 10: 63.65 / 22.24 / 16.19, 20: 63.12 / 21.86 / 14.96
+    const int pd = c->opt.probe_depth >= 0 ? c->opt.probe_depth : ((vmask & F_STEP) != 0 ? 10 : 20);
+    if (pd > 0) Q.max_depth = std::min(a->max_depth, pd);
     Q.total_items = (unsigned long long)pitems;
     Q.pstep = ps;
     Q.per_row = pw;
