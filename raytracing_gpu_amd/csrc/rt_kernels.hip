@@ -1895,6 +1895,23 @@ constexpr int render_wpe() {
   return (F & F_LDS) != 0 ? 1
                           : (feat == F_FINAL || feat == F_MESH ? 4 : (feat == F_CORNELL ? 5 : (feat == F_ALL ? 3 : 1)));
 }
+// The kernel arguments through an opaque pointer to the kernarg segment, once per loop trip: their
+// fields are then re-read (scalar loads) in every trip instead of held in SGPRs across the whole loop.
+// Only in the list variants without BVHs or triangles (C3's): their SGPR spills 64 -> 0 and VGPR spills
+// 16 -> 8, 1.8-2.7 % faster (same box, profiles/r06/launder_ab.txt); the other variants measured slower
+// with it (C2's stepwise 6.5 %, C4 1.4 %, C5 0.5 %: the reloads sit in their dependent chains).
+template <int F>
+constexpr bool launders() { return (F & (F_BVH | F_TRI)) == 0; }
+template <int F>
+__device__ __forceinline__ const RenderParams& loop_params(const RenderParams& P0) {
+  if constexpr (launders<F>()) {
+    const RT_RO RenderParams* p = (const RT_RO RenderParams*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const RenderParams*)p;
+  } else {
+    return P0;
+  }
+}
 template <int F>
 __global__ __launch_bounds__(render_block<F>()) __attribute__((amdgpu_waves_per_eu(render_wpe<F>())))
 void render_kernel(const RenderParams P) {
@@ -1969,7 +1986,12 @@ void render_kernel(const RenderParams P) {
   unsigned long long chunk_base = 0;  // wave-uniform: next unclaimed item of the wave's chunk
   unsigned chunk_left = 0;
 
+  const RenderParams& P0 = P;
   for (;;) {
+    // the kernel arguments re-read every loop trip in the variants that launder them (loop_params)
+    const RenderParams& P = loop_params<F>(P0);
+    const DScene& S = P.S;
+    const rt_camera& C = S.cam;
     // ---- refill idle lanes (one atomic per wave, ballot-compacted ranks)
     RT_STAMP(7);  // back-to-back pair: phase 7 = the cost of one stamp per loop trip
     RT_STAMP(0);
