@@ -3500,7 +3500,7 @@ __global__ __launch_bounds__(64) void key_base_kernel(const unsigned* __restrict
 // Item schedule of a configuration from its measuring launch's per-item segment counts (c->item_cost,
 // `segs` segments in all): perm, the long prefix and the split items.  Built when the configuration
 // is rendered again, so a single draw() does not pay the host sort.
-int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs) {
+int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs, bool step_kernel) {
   RT_DIAG_ITEM_COSTS(c, items);  // diagnostic builds only (rt_diag.h): per-item segment counts to a file
   // Every item in descending cost buckets of 8 segments, the natural (spatially coherent) order
   // inside a bucket (a stable counting sort on the device; the top bucket 255 holds every item of
@@ -3520,8 +3520,12 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
     HIPCHK(c, hipMemcpyAsync(&cmax, dmax, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
-  int shift = 3;
-  while (shift < 8 && (cmax >> shift) > 255u) ++shift;
+  // (render_kernel: exact counts, buckets of one segment, the longest quarter of the range saturating the
+  // top bucket.  Its waves refill once 4 lanes are idle, and items of equal cost in a wave end together:
+  // C5 warm 55.0 -> 51.8 ms per launch at N = 1, 7.86 -> 6.96 at N = 8 (profiles/r06/cost_shift/); the
+  // stepwise kernel, which refills every idle lane, keeps buckets of 8)
+  int shift = step_kernel ? 3 : 0;
+  while (shift < 8 && (cmax >> shift) > (step_kernel ? 255u : 1023u)) ++shift;
   if (c->opt.cost_shift >= 0) shift = std::min(12, c->opt.cost_shift);  // tuning
   cost_key_kernel<<<(unsigned)((items + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
       c->item_cost, (unsigned long long)items, shift, keys);
@@ -3595,10 +3599,14 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs)
 // long_pct % of the positions.  Cost buckets of 8 segments, as the measured schedule's (natural order
 // inside a bucket keeps neighbouring claims coherent), wider where smoothed means of up to 32 segments
 // per sample would saturate the top bucket (a grid point above that, rare, saturates it).
-int probe_schedule(rt_ctx* c, long long items, int spp, int width, int fbc, int ps, int pw, long long pitems) {
+int probe_schedule(rt_ctx* c, long long items, int spp, int width, int fbc, int ps, int pw, long long pitems,
+                   bool step_kernel) {
   uint8_t* keys = sort_keys(c, items);
   if (!keys) return fail(c, RT_ERR_HIP, "out of device memory (probe schedule)");
-  int shift = 3;
+  // (render_kernel: buckets of 2 segments.  C5 first launches at N = 1 / 2 / 4 / 8, buckets of 8 / 4 / 2 /
+  // 1: 63.2 / 63.1 / 63.0 / 64.4 ms, 35.9 / 33.8 / 34.0 / 34.4, 22.1 / 20.4 / 20.2 / 20.3, 14.8 / 15.2 /
+  // 14.5 / 14.4; profiles/r06/cost_shift/)
+  int shift = step_kernel ? 3 : 1;
   while (shift < 12 && ((32LL * spp) >> shift) > 255) ++shift;
   if (c->opt.cost_shift >= 0) shift = c->opt.cost_shift;  // tuning
   probe_keys_kernel<<<(unsigned)std::min<long long>(4096, (items + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
@@ -4392,6 +4400,8 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   // cam_mode is part of the key: the split samples' recorded sample-start states depend on it (the
   // PER_PIXEL camera draws come from the pixel's own state, REF ones from the slot-0 copy)
   constexpr int K = rt_ctx::kKey;
+  // the launch runs render_step_kernel (as pick_variant decides below): the schedules' cost buckets
+  const bool step_kernel = (c->world_step || c->world_tree) && (a->flags & (RT_FLAG_NO_STEP | RT_FLAG_WIDEST)) == 0;
   const long long pkey[K] = {c->scene_gen, a->width,   a->height,    a->spp,       a->max_depth, a->fb_first,
                              a->fb_count,  a->band_rows, a->band_first, a->band_stride, a->cam_mode};
   // (up to 2^31 items: 6 bytes of cost and position per item, C5's configured 100 fb x 100 spp draw
@@ -4406,7 +4416,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
   }
   if (sched && !std::equal(pkey, pkey + K, c->perm_key) && std::equal(pkey, pkey + K, c->pending_key) &&
       items <= c->item_cap) {  // the configuration repeats: its schedule from the measured counts
-    if ((rc = build_schedule(c, items, a->spp, c->pending_segs))) return rc;
+    if ((rc = build_schedule(c, items, a->spp, c->pending_segs, step_kernel))) return rc;
     std::copy(pkey, pkey + K, c->perm_key);
     std::fill(c->pending_key, c->pending_key + K, -1LL);
   }
@@ -4767,7 +4777,7 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     c->split_state = -1;
     c->n_split = 0;
     c->order_ok = false;
-    if ((rc = probe_schedule(c, items, a->spp, a->width, a->fb_count, ps, pw, pitems))) return rc;
+    if ((rc = probe_schedule(c, items, a->spp, a->width, a->fb_count, ps, pw, pitems, step_kernel))) return rc;
     P.perm = c->perm;
     P.n_long = c->n_long;
   }
