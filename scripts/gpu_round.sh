@@ -56,6 +56,7 @@ for s in ${STEPS:-tests smoke c2}; do
     osweep_*)  # scripts/diag_scale.py per context option setting: OSWEEP="probe_depth=0 probe_depth=8" STEPS=osweep_c2
       w=${s#osweep_}
       case $w in c2) wl="big1 1200 800 10 10";; c2x100) wl="big1 1200 800 100 1";; c4) wl="door 1920 1079 16 16";;
+                 c3) wl="cornell_smoke 800 800 10 10";;
                  c5) wl="final 3840 2159 4 4";; *) echo "unknown workload $w"; exit 2;; esac
       for o in ${OSWEEP:-probe_depth=0}; do
         run osweep_${w}_${o//[=.,]/_} 600 python -u scripts/diag_scale.py $wl $(echo ",$o" | sed 's/,/ --opt /g') || exit $?

@@ -164,3 +164,58 @@ def test_final_high_fb_ids_at_full_size(rtlib, gpu_ctx, oracle, cam):
         q = [pos[j] for j in js]
         for f in range(nfb):
             assert np.array_equal(_bits(got[f][q]), _bits(want[f][js])), f"launch {launch} fb id {first + f}"
+
+
+@pytest.mark.parametrize("depth", [0, 3, -1], ids=["full", "3", "auto"])
+@pytest.mark.parametrize("scene", ["big1", "door", "final"])
+def test_probe_depth_bit_exact(rtlib, gpu_ctx, ctx_opts, oracle, scene, depth):
+    """options.probe_depth cuts a probe sample's path (the probe launch's output is discarded, its counts
+    only order the items): the first launch equals the oracle bit for bit at every cap, on the stepwise
+    kernel (big1, door) and on render_kernel's merged variant (final); the probe runs under the F_PROBE
+    twin's symbol, and rt_last_kernel_ms times the render kernel alone (inside rt_last_render_ms)."""
+    W, H, spp, nfb = 96, 54, 4, 2
+    pa, oa = {}, {}
+    if scene != "big1":
+        from raytracing_gpu_amd import assets
+
+        m = assets.door_mesh_from_fixture(os.path.join(GOLD, "door_assimp.npz"))
+        img = assets.synthetic_image(341, 152)
+        pa, oa = dict(images=[img], meshes=[m]), dict(images=[img], meshes=[(m.tris, True, 0)])
+    ctx_opts(probe_depth=depth)
+    gpu_ctx.upload(rtlib.Scene.builtin(scene, **pa))
+    want = _big1_frames(W, H, spp, nfb, REF) if scene == "big1" else [
+        oracle.RefScene(scene, **oa).render(W, H, spp, f, 50, REF)[0].reshape(H, W, 3) for f in range(nfb)]
+    got, rows, cnt, sched = _launch(rtlib, gpu_ctx, W, H, spp, nfb, REF, fresh=True)
+    assert sched == rtlib.RT_SCHED_PROBE
+    name = gpu_ctx.last_render_kernel()
+    assert not int(name.split("<")[1].rstrip(">")) & (1 << 18), name  # the render kernel, not its probe twin
+    assert 0 < gpu_ctx.last_kernel_ms() <= gpu_ctx.last_render_ms()
+    for f in range(nfb):
+        assert np.array_equal(_bits(got[f]), _bits(want[f])), f"{scene} depth {depth} fb {f}"
+
+
+def test_stats_twin_of_the_stepwise_variant(rtlib, gpu_ctx, oracle):
+    """bench.py's counting pass runs the F_STATS twin of C2's stepwise LDS variant (the traversal that is
+    timed, camera tile lists included): same frame buffers and segment count as the product launch, the
+    oracle's pixels, and fewer node tests than the reference's exact visit set."""
+    import torch
+
+    W, H, spp, nfb = 160, 90, 2, 2
+    gpu_ctx.upload(rtlib.Scene.builtin("big1"))
+    out = {}
+    for mode in ("product", "stats", "exact"):
+        gpu_ctx.render_init(W, H, 1984)
+        fb = torch.zeros(nfb * H * W * 3, dtype=torch.float32, device="cuda")
+        args = rtlib.make_args(W, H, spp, 0, nfb, 50, REF, stats=mode != "product", exact=mode == "exact",
+                               schedule=False)
+        cnt = gpu_ctx.render(args, fb.data_ptr())
+        out[mode] = (fb.cpu().numpy(), cnt, gpu_ctx.last_render_kernel())
+    assert out["product"][2] == "render_step_kernel<25730>", out["product"][2]
+    assert out["stats"][2] == "render_step_kernel<25731>", out["stats"][2]
+    assert out["stats"][1]["segments"] == out["product"][1]["segments"] == out["exact"][1]["segments"]
+    assert np.array_equal(_bits(out["stats"][0]), _bits(out["product"][0]))
+    assert 0 < out["stats"][1]["node_tests"] < out["exact"][1]["node_tests"]
+    want = _big1_frames(W, H, spp, nfb, REF)
+    got = out["stats"][0].reshape(nfb, H, W, 3)
+    for f in range(nfb):
+        assert np.array_equal(_bits(got[f]), _bits(want[f]))
