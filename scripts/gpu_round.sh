@@ -51,6 +51,7 @@ for s in ${STEPS:-tests smoke c2}; do
     scale_c5) run scale_c5 600 python -u scripts/diag_scale.py final 3840 2159 4 4 ${SCALE_OPTS:-} || exit $? ;;
     scale_c2x100) run scale_c2x100 600 python -u scripts/diag_scale.py big1 1200 800 100 1 ${SCALE_OPTS:-} || exit $? ;;
     trace_c2) NAME=c2 bash scripts/trace_cold.sh || exit $? ;;
+    btrace_c2) NAME=c2 bash scripts/trace_bench.sh || exit $? ;;
     trace_c4) NAME=c4 ARGS="--scene door --width 1920 --height 1079 --spp 16 --nfb 16" bash scripts/trace_cold.sh || exit $? ;;
     trace_c5) NAME=c5 ARGS="--scene final --width 3840 --height 2159 --spp 4 --nfb 4" bash scripts/trace_cold.sh || exit $? ;;
     osweep_*)  # scripts/diag_scale.py per context option setting: OSWEEP="probe_depth=0 probe_depth=8" STEPS=osweep_c2
