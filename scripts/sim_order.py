@@ -71,6 +71,8 @@ def main():
         report("natural", np.arange(items))
         report("true cost, exact", stable_desc(cost))
         report("true cost, 8-segment buckets", stable_desc(np.minimum(cost >> 3, 255)))
+        pix = cost.reshape(rows, nfb, W).mean(axis=1)  # the best any per-pixel estimate can know
+        report("pixel mean of true costs (per-pixel ceiling)", stable_desc(np.round(pix[q, i] * 16).astype(np.int64)))
         for ps in (1, 2, 4):
             sub = raw[::ps, ::ps]
             for depth in (0, 10):

@@ -81,7 +81,8 @@ def test_bad_options_are_rejected(rtlib, gpu_ctx):
     keeps the previous options."""
     before = gpu_ctx.options()
     for bad in (dict(cost_shift=-2), dict(cost_shift=13), dict(world_tree=2), dict(quantized_tree=-1),
-                dict(dedup_triangles=3), dict(split_order=2), dict(shade_min=65), dict(probe_schedule=-2)):
+                dict(dedup_triangles=3), dict(split_order=2), dict(shade_min=65), dict(probe_schedule=-2),
+                dict(probe_depth=-2)):
         with pytest.raises(rtlib.RtError):
             gpu_ctx.set_options(**bad)
         assert gpu_ctx.options() == before, bad
