@@ -265,6 +265,10 @@ typedef struct rt_ctx_options {
   int32_t probe_depth;       /* k > 0: a probe sample's path ends after k segments (the probe launch
                                 lasts as long as its longest path); 0: the launch's max_depth; -1
                                 (default): 10 for the stepwise kernel, 20 for the others            */
+  int32_t spread_first;      /* k = 1..64: a probe-ordered first launch gives each wave's first
+                                claim k of the order's first k x waves items, strided (one wave
+                                does not start with many of the longest), and 64 - k neighbours
+                                in order; 0: the order as is; -1 (default): automatic              */
 } rt_ctx_options;
 void rt_ctx_options_default(rt_ctx_options* opts);
 int rt_ctx_set_options(rt_ctx* ctx, const rt_ctx_options* opts);

@@ -104,7 +104,8 @@ class rt_ctx_options(ctypes.Structure):
                 ("merge_order", c_int32), ("dedup_triangles", c_int32), ("shade_min", c_int32),
                 ("bins_min_items_per_lane", c_float), ("split_min_segments", c_float), ("split_order", c_int32),
                 ("cost_shift", c_int32), ("long_pct", c_float), ("probe_schedule", c_int32),
-                ("probe_max_items_per_lane", c_float), ("probe_depth", c_int32)]
+                ("probe_max_items_per_lane", c_float), ("probe_depth", c_int32),
+                ("spread_first", c_int32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

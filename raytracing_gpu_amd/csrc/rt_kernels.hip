@@ -2971,6 +2971,8 @@ struct rt_ctx {
   uint16_t* item_cost = nullptr;
   uint16_t* probe_cost = nullptr;  // per (owned row, pixel): the probe launch's segment counts
   long long probe_cap = 0;
+  uint32_t* spread_tmp = nullptr;  // probe_schedule: a copy of perm's head, gathered back spread
+  long long spread_cap = 0;
   uint32_t* perm = nullptr;
   long long item_cap = 0;
   static constexpr int kKey = 11;
@@ -3593,6 +3595,19 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs,
   return RT_OK;
 }
 
+// Position k < 64 * nw of chunk c = k / 64, lane l = k % 64 takes rank l * nw + c of the head (a copy of
+// perm's first 64 * nw entries) for l < top, else rank top * nw + c * (64 - top) + l - top: the chunk of 64
+// positions a wave claims first holds `top` items strided over the head's first top * nw ranks and
+// 64 - top consecutive ones (neighbours in the order, spatially coherent inside a cost bucket).
+__global__ __launch_bounds__(kBlock) void spread_head_kernel(const uint32_t* __restrict__ head, uint32_t* __restrict__ perm,
+                                                             unsigned long long nw, unsigned top) {
+  for (unsigned long long k = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; k < 64ull * nw;
+       k += (unsigned long long)gridDim.x * blockDim.x) {
+    const unsigned long long c = k >> 6, l = k & 63ull;
+    perm[k] = head[l < top ? l * nw + c : top * nw + c * (64ull - top) + l - top];
+  }
+}
+
 // Item schedule of a probe-scheduled first launch from the smoothed probe grid (c->probe_cost + pitems):
 // every step on the device, no host round trip (the draw's critical path): per-item keys, the tile
 // histograms and their scan, the bases, the stable scatter into perm.  The long prefix is the first
@@ -3600,7 +3615,7 @@ int build_schedule(rt_ctx* c, long long items, int spp, unsigned long long segs,
 // inside a bucket keeps neighbouring claims coherent), wider where smoothed means of up to 32 segments
 // per sample would saturate the top bucket (a grid point above that, rare, saturates it).
 int probe_schedule(rt_ctx* c, long long items, int spp, int width, int fbc, int ps, int pw, long long pitems,
-                   bool step_kernel) {
+                   bool step_kernel, long long waves, int spread_top) {
   uint8_t* keys = sort_keys(c, items);
   if (!keys) return fail(c, RT_ERR_HIP, "out of device memory (probe schedule)");
   // (render_kernel: buckets of 2 segments.  C5 first launches at N = 1 / 2 / 4 / 8, buckets of 8 / 4 / 2 /
@@ -3623,6 +3638,24 @@ int probe_schedule(rt_ctx* c, long long items, int spp, int width, int fbc, int 
   HIPCHK(c, hipGetLastError());
   if (int rc = sort_scatter(c, items, c->order_tab, c->perm)) return rc;
   c->n_long = (unsigned long long)((double)items * c->opt.long_pct / 100.0);
+  // Spread head (spread_top > 0, options.spread_first): longest first, the first claims would hand the
+  // estimated-longest items 64 to a wave to the waves that claim first (one workgroup's); strided, every
+  // wave starts with spread_top of the head's first spread_top * waves items
+  const int sf = spread_top;
+  if (sf > 0 && waves > 0 && items >= 64 * waves) {
+    const long long n = 64 * waves;
+    if (n > c->spread_cap) {
+      if (c->spread_tmp) HIPCHK(c, hipFree(c->spread_tmp));
+      c->spread_tmp = nullptr;
+      c->spread_cap = 0;
+      HIPCHK(c, hipMalloc((void**)&c->spread_tmp, (size_t)n * sizeof(uint32_t)));
+      c->spread_cap = n;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->spread_tmp, c->perm, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+    spread_head_kernel<<<(unsigned)std::min<long long>(4096, (n + kBlock - 1) / kBlock), kBlock, 0, c->stream>>>(
+        c->spread_tmp, c->perm, (unsigned long long)waves, (unsigned)sf);
+    HIPCHK(c, hipGetLastError());
+  }
   return RT_OK;
 }
 
@@ -3712,6 +3745,7 @@ int rt_ctx_destroy(rt_ctx* c) {
   if (c->row_cost) (void)hipFree(c->row_cost);
   if (c->item_cost) (void)hipFree(c->item_cost);
   if (c->probe_cost) (void)hipFree(c->probe_cost);
+  if (c->spread_tmp) (void)hipFree(c->spread_tmp);
   if (c->perm) (void)hipFree(c->perm);
   if (c->dbg) (void)hipFree(c->dbg);
   if (c->tiles) (void)hipFree(c->tiles);
@@ -3749,6 +3783,7 @@ void rt_ctx_options_default(rt_ctx_options* o) {
   o->probe_schedule = -1;
   o->probe_max_items_per_lane = 0.0f;
   o->probe_depth = -1;
+  o->spread_first = -1;
 }
 
 int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
@@ -3759,7 +3794,8 @@ int rt_ctx_set_options(rt_ctx* c, const rt_ctx_options* o) {
       o->cost_shift < -1 || o->cost_shift > 12 || !(o->long_pct >= 0.0f && o->long_pct <= 100.0f) ||
       o->probe_schedule < -1 || o->probe_schedule > 64 || !(o->probe_max_items_per_lane >= 0.0f) ||
       (o->world_tree & ~1) != 0 || (o->quantized_tree & ~1) != 0 || (o->dedup_triangles & ~1) != 0 ||
-      (o->split_order & ~1) != 0 || o->probe_depth < -1)
+      (o->split_order & ~1) != 0 || o->probe_depth < -1 || o->spread_first < -1 ||
+      o->spread_first > 64)
     return fail(c, RT_ERR_ARG, "bad context options");
   c->opt = *o;
   // the schedule and split thresholds come from the options: every configuration starts cold again
@@ -4777,7 +4813,17 @@ int render_dev(rt_ctx* c, const rt_render_args* a, float* fb_dev, rt_counters* c
     c->split_state = -1;
     c->n_split = 0;
     c->order_ok = false;
-    if ((rc = probe_schedule(c, items, a->spp, a->width, a->fb_count, ps, pw, pitems, step_kernel))) return rc;
+    // spread head (automatic: the stepwise triangle-mesh variants, every position of the first claims
+    // strided).  Measured (MI355X, one GPU rendering each rank's share, first launches, ms at N = 1 / 2 /
+    // 4 / 8; profiles/r06/spread/): C4 in order 65.54 / 36.87 / 24.42 / 24.20, spread 1 65.53 / 36.79 /
+    // 24.61 / 23.93, 8 65.45 / 36.92 / 24.43 / 19.10, 64 65.56 / 36.89 / 24.64 / 18.33; C2 in order 16.77 /
+    // 9.06 / 5.76 / 3.96, 1 16.74 / 9.09 / 5.46 / 3.99, 64 16.89 / 9.26 / 5.89 / 4.44 (its waves lose the
+    // coherence of neighbouring items)
+    const int spread_top =
+        c->opt.spread_first >= 0 ? c->opt.spread_first : (step_kernel && (vmask & F_TRI) != 0 ? 64 : 0);
+    if ((rc = probe_schedule(c, items, a->spp, a->width, a->fb_count, ps, pw, pitems, step_kernel,
+                             (long long)blocks * (bs / 64), spread_top)))
+      return rc;
     P.perm = c->perm;
     P.n_long = c->n_long;
   }

@@ -82,7 +82,7 @@ def test_bad_options_are_rejected(rtlib, gpu_ctx):
     before = gpu_ctx.options()
     for bad in (dict(cost_shift=-2), dict(cost_shift=13), dict(world_tree=2), dict(quantized_tree=-1),
                 dict(dedup_triangles=3), dict(split_order=2), dict(shade_min=65), dict(probe_schedule=-2),
-                dict(probe_depth=-2)):
+                dict(probe_depth=-2), dict(spread_first=-2), dict(spread_first=65)):
         with pytest.raises(rtlib.RtError):
             gpu_ctx.set_options(**bad)
         assert gpu_ctx.options() == before, bad
@@ -220,3 +220,37 @@ def test_stats_twin_of_the_stepwise_variant(rtlib, gpu_ctx, oracle):
     got = out["stats"][0].reshape(nfb, H, W, 3)
     for f in range(nfb):
         assert np.array_equal(_bits(got[f]), _bits(want[f]))
+
+
+@pytest.mark.parametrize("spread", [1, 7, 64])
+@pytest.mark.parametrize("scene", ["big1", "door"])
+def test_spread_head_bit_exact(rtlib, gpu_ctx, ctx_opts, oracle, scene, spread):
+    """options.spread_first: a probe-ordered first launch hands its first 64 x waves positions out strided
+    (spread_head_kernel).  Large enough that it applies (items >= 64 x the launch's waves: 16 waves per
+    workgroup, one workgroup per CU), the launch equals the natural-order launch (RT_FLAG_NO_SCHEDULE)
+    bit for bit with the same segment count, every item claimed once; a row subset against the oracle."""
+    import torch
+
+    W, H, spp, nfb = 640, 360, 2, 2
+    assert nfb * W * H >= 64 * 16 * torch.cuda.get_device_properties(0).multi_processor_count
+    pa, oa = {}, {}
+    if scene != "big1":
+        from raytracing_gpu_amd import assets
+
+        m = assets.door_mesh_from_fixture(os.path.join(GOLD, "door_assimp.npz"))
+        img = assets.synthetic_image(341, 152)
+        pa, oa = dict(images=[img], meshes=[m]), dict(images=[img], meshes=[(m.tris, True, 0)])
+    ctx_opts(spread_first=spread)
+    gpu_ctx.upload(rtlib.Scene.builtin(scene, **pa))
+    base, _, bcnt, s0 = _launch(rtlib, gpu_ctx, W, H, spp, nfb, REF, schedule=False)
+    assert s0 == 0
+    got, rows, cnt, sched = _launch(rtlib, gpu_ctx, W, H, spp, nfb, REF, fresh=True)
+    assert sched == rtlib.RT_SCHED_PROBE
+    assert cnt["segments"] == bcnt["segments"] and cnt["samples"] == nfb * W * H * spp
+    assert np.array_equal(_bits(got), _bits(base)), f"{scene} spread {spread}"
+    sub = (5, 41)
+    js = list(range(sub[0], H, sub[1]))
+    ref = oracle.RefScene(scene, **oa)
+    for f in range(nfb):
+        want = ref.render(W, H, spp, f, 50, REF, rows=sub)[0].reshape(H, W, 3)
+        assert np.array_equal(_bits(got[f][js]), _bits(want[js])), f"{scene} spread {spread} fb {f}"
